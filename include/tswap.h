@@ -1,0 +1,147 @@
+/*
+ * tswap.h — C ABI of the MI355X-native TSWAP planning core (libtswap_hip.so).
+ *
+ * Drop-in boundary for the reference's src/algorithm path
+ * (RenKoya1/p2p_distributed_tswap @ 2025-11-21). Plain pointers and sizes,
+ * no torch types. Every call is synchronous for the caller (like the
+ * reference); device work runs on the context's own HIP stream.
+ *
+ * Coordinates: Point = (x, y) with x = column, y = row, grid[y][x]
+ * (src/map/map.rs:4, tswap.rs:53). Cell id = y*w + x. A cell is blocked iff
+ * its byte is '@' (tswap.rs:53); every other byte is passable.
+ *
+ * Errors: 0 on success, negative errno-style code otherwise; the reference
+ * panics where these return TSW_EINVAL (tswap.rs:94,112,136).
+ * tsw_last_error(ctx) gives the message of the last failure.
+ * One context is single-threaded; separate contexts may live on separate
+ * threads or devices.
+ */
+#ifndef TSWAP_H
+#define TSWAP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSW_OK 0
+#define TSW_EINVAL (-22)
+#define TSW_ENOMEM (-12)
+#define TSW_EHIP (-5)
+#define TSW_EOVERFLOW (-75)
+#define TSW_ENODEV (-19)
+
+/* AgentState discriminants in declaration order (src/map/agent.rs:9-15) */
+#define TSW_PICKING 0
+#define TSW_CARRYING 1
+#define TSW_DELIVERED 2
+#define TSW_IDLE 3
+
+/* Sentinel distance in tables: blocked or unreachable cell. */
+#define TSW_DIST_INF 0xFFFFu
+
+typedef struct tsw_ctx tsw_ctx;
+
+/* src/map/map.rs:4 `pub type Point = (usize, usize)` */
+typedef struct {
+    uint32_t x, y;
+} tsw_point;
+
+/* src/map/task_generator.rs:6-12 `Task{pickup, delivery, peer_id, task_id}`;
+ * peer_id/task_id are never read by the planner and are not carried. */
+typedef struct {
+    tsw_point pickup, delivery;
+} tsw_task;
+
+/* One element of tswap_mapd's Vec<Vec<(Point, AgentState)>> (tswap.rs:43). */
+typedef struct {
+    uint16_t x, y;
+    uint8_t state; /* TSW_PICKING .. TSW_IDLE */
+    uint8_t pad[3];
+} tsw_rec;
+
+typedef struct {
+    int32_t device;              /* HIP device ordinal (default 0)             */
+    uint32_t flags;              /* TSW_F_* below                              */
+    uint64_t table_budget_bytes; /* cap for distance+next-hop tables (0=auto)  */
+} tsw_opts;
+
+/* Resolve every multi-candidate next hop of every table eagerly (one big
+ * batched A* pass right after the BFS tables) instead of lazily per step. */
+#define TSW_F_EAGER_NEXTHOP 1u
+/* Never eager (lazy only), even when the auto policy would pick eager. */
+#define TSW_F_LAZY_NEXTHOP 2u
+
+/* Replaces the graph build of tswap_mapd (tswap.rs:44-77) and of the
+ * centralized manager (bin/centralized/manager.rs:503-535): uploads the grid
+ * and builds the device neighbour masks. cells: h rows of w bytes.
+ * opts may be NULL. Returns NULL on failure (see tsw_last_error(NULL)). */
+tsw_ctx *tsw_create(const uint8_t *cells, uint32_t w, uint32_t h, const tsw_opts *opts);
+void tsw_destroy(tsw_ctx *ctx);
+/* Message of the last failure on ctx (ctx may be NULL: last create failure). */
+const char *tsw_last_error(const tsw_ctx *ctx);
+
+/* Replaces `tswap_mapd(grid, initial_positions, tasks)` (tswap.rs:39-172).
+ * out: caller-allocated n*(max_t+1) records, agent-major:
+ *   out[i*(max_t+1) + t] == paths[i][t]  for t < *out_T.
+ * max_t = 2000 reproduces the reference's `timestep > 2000` stop (:167).
+ * Returns TSW_EINVAL if a start, pickup or delivery is off-grid or blocked. */
+int tsw_plan_mapd(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const tsw_task *tasks,
+                  uint32_t m, uint32_t max_t, tsw_rec *out, uint32_t *out_T);
+
+/* As tsw_plan_mapd, additionally writing the goal cell id of every agent after
+ * each step (same layout as out) — a debug trace for parity localisation.
+ * goal_out may be NULL. */
+int tsw_plan_mapd_trace(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const tsw_task *tasks,
+                        uint32_t m, uint32_t max_t, tsw_rec *out, uint32_t *goal_out,
+                        uint32_t *out_T);
+
+/* Replaces one `tswap_step(&mut agents, &nodes)` call (tswap.rs:174-286;
+ * per-tick copy in bin/centralized/manager.rs:147-259 via plan_all_paths
+ * :101-144). v[i], g[i]: cell ids in/out, agent order = array order. */
+int tsw_step(tsw_ctx *ctx, uint32_t *v, uint32_t *g, uint32_t n);
+
+/* Batched `get_path(start, goal)` (tswap.rs:288-390), reduced to what every
+ * caller consumes: next[q] = path[1] (start if len==1) and len[q] = len(path)
+ * (1: start==goal, 2: unreachable fallback or adjacent goal, D+1 otherwise). */
+int tsw_get_path_next(tsw_ctx *ctx, const uint32_t *start, const uint32_t *goal, uint32_t k,
+                      uint32_t *next, int32_t *len);
+
+/* K1: BFS distance tables for k goal cells, u16 per cell, row-major
+ * (TSW_DIST_INF for blocked/unreachable). out: host buffer k*w*h. */
+int tsw_dist_tables(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint16_t *out);
+
+/* K1 into caller-owned DEVICE memory (e.g. a torch tensor's data_ptr on the
+ * context's device): dev_out receives k*w*h u16. Used for goal-sharded
+ * construction + RCCL all-gather. */
+int tsw_dist_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint16_t *dev_out);
+
+/* Ingest k tables (k*w*h u16, DEVICE memory, e.g. the all-gather result)
+ * into the context's table store so steps use them without recomputing. */
+int tsw_import_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k,
+                             const uint16_t *dev_tables);
+
+/* Per-context counters and kernel timings (HIP events on the context stream). */
+typedef struct {
+    uint64_t bfs_goals, bfs_launches;
+    double bfs_ms;              /* summed K1 kernel time                     */
+    uint64_t astar_queries, astar_launches;
+    double astar_ms;            /* summed K3 kernel time                     */
+    uint64_t walker_launches;   /* K2 serial-commit launches                 */
+    double walker_ms;
+    uint64_t assign_launches;
+    double assign_ms;
+    uint64_t steps;             /* timesteps planned                         */
+    uint64_t tables;            /* goal tables resident                      */
+    double plan_ms;             /* wall time of the last plan call           */
+} tsw_stats;
+int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
+int tsw_reset_stats(tsw_ctx *ctx);
+/* Enable/disable HIP-event timing around kernels (default on). */
+int tsw_set_timing(tsw_ctx *ctx, int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,291 @@
+"""MI355X-native TSWAP planning core — Python mirror of the reference interface.
+
+Drop-in for the src/algorithm path of RenKoya1/p2p_distributed_tswap
+(@ 2025-11-21). Everything here is a thin ctypes layer over the C ABI in
+include/tswap.h (libtswap_hip.so: hand-written gfx950 HIP kernels + C++ host
+runtime). There is NO CPU fallback: if the HIP library or a GPU is missing,
+every call raises.
+
+Reference interface mirrored (same names, argument meaning, error behaviour):
+  tswap_mapd(grid, initial_positions, tasks)  src/algorithm/tswap.rs:39-43
+      -> list[list[((x, y), AgentState)]]; panics become TswapError(EINVAL)
+  AgentState                                  src/map/agent.rs:9-15
+  Task(pickup, delivery, peer_id, task_id)    src/map/task_generator.rs:6-12
+  Point = (x, y)                              src/map/map.rs:4
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+from dataclasses import dataclass
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+__all__ = [
+    "AgentState", "Task", "TswapError", "Planner", "tswap_mapd", "tswap_step",
+    "load_library", "LIB_PATH", "grid_to_bytes",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtswap_hip.so")
+
+TSW_OK, TSW_EINVAL, TSW_ENOMEM, TSW_EHIP, TSW_EOVERFLOW = 0, -22, -12, -5, -75
+TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP = 1, 2
+DIST_INF = 0xFFFF
+
+
+class AgentState(enum.IntEnum):
+    """src/map/agent.rs:9-15 (discriminants in declaration order)."""
+    PICKING = 0
+    CARRYING = 1
+    DELIVERED = 2
+    IDLE = 3
+
+
+@dataclass
+class Task:
+    """src/map/task_generator.rs:6-12. peer_id/task_id are carried, never read by the planner."""
+    pickup: tuple
+    delivery: tuple
+    peer_id: Optional[str] = None
+    task_id: Optional[int] = None
+
+
+class TswapError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"tswap error {code}: {msg}")
+        self.code = code
+
+
+class _Point(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_uint32), ("y", ctypes.c_uint32)]
+
+
+class _Task(ctypes.Structure):
+    _fields_ = [("pickup", _Point), ("delivery", _Point)]
+
+
+class _Rec(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_uint16), ("y", ctypes.c_uint16), ("state", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8 * 3)]
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("table_budget_bytes", ctypes.c_uint64)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("bfs_goals", ctypes.c_uint64), ("bfs_launches", ctypes.c_uint64), ("bfs_ms", ctypes.c_double),
+        ("astar_queries", ctypes.c_uint64), ("astar_launches", ctypes.c_uint64), ("astar_ms", ctypes.c_double),
+        ("walker_launches", ctypes.c_uint64), ("walker_ms", ctypes.c_double),
+        ("assign_launches", ctypes.c_uint64), ("assign_ms", ctypes.c_double),
+        ("steps", ctypes.c_uint64), ("tables", ctypes.c_uint64), ("plan_ms", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# every symbol declared in include/tswap.h (tests check the .so exports them)
+EXPORTED_SYMBOLS = (
+    "tsw_create", "tsw_destroy", "tsw_last_error", "tsw_plan_mapd", "tsw_plan_mapd_trace",
+    "tsw_step", "tsw_get_path_next", "tsw_dist_tables", "tsw_dist_tables_device",
+    "tsw_import_tables_device", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing",
+)
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libtswap_hip.so (built by __graft_entry__.build()). Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise TswapError(TSW_EHIP, f"HIP library not built: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    u32, i32, u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
+    vp = ctypes.c_void_p
+    lib.tsw_create.argtypes = [P(ctypes.c_uint8), u32, u32, P(_Opts)]
+    lib.tsw_create.restype = vp
+    lib.tsw_destroy.argtypes = [vp]
+    lib.tsw_destroy.restype = None
+    lib.tsw_last_error.argtypes = [vp]
+    lib.tsw_last_error.restype = ctypes.c_char_p
+    lib.tsw_plan_mapd.argtypes = [vp, P(_Point), u32, P(_Task), u32, u32, P(_Rec), P(u32)]
+    lib.tsw_plan_mapd_trace.argtypes = [vp, P(_Point), u32, P(_Task), u32, u32, P(_Rec), P(u32), P(u32)]
+    lib.tsw_step.argtypes = [vp, P(u32), P(u32), u32]
+    lib.tsw_get_path_next.argtypes = [vp, P(u32), P(u32), u32, P(u32), P(i32)]
+    lib.tsw_dist_tables.argtypes = [vp, P(u32), u32, P(ctypes.c_uint16)]
+    lib.tsw_dist_tables_device.argtypes = [vp, P(u32), u32, vp]
+    lib.tsw_import_tables_device.argtypes = [vp, P(u32), u32, vp]
+    lib.tsw_get_stats.argtypes = [vp, P(Stats)]
+    lib.tsw_reset_stats.argtypes = [vp]
+    lib.tsw_set_timing.argtypes = [vp, ctypes.c_int]
+    for name in ("tsw_plan_mapd", "tsw_plan_mapd_trace", "tsw_step", "tsw_get_path_next", "tsw_dist_tables",
+                 "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_get_stats", "tsw_reset_stats",
+                 "tsw_set_timing"):
+        getattr(lib, name).restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def grid_to_bytes(grid) -> tuple:
+    """grid: list[str] | list[list[str]] | np.ndarray(uint8, HxW). Returns (bytes_array, w, h).
+
+    Mirrors the reference: h = len(grid), w = len(grid[0]) (tswap.rs:46-47).
+    """
+    if isinstance(grid, np.ndarray):
+        a = np.ascontiguousarray(grid, dtype=np.uint8)
+        return a, a.shape[1], a.shape[0]
+    rows = ["".join(r) if not isinstance(r, str) else r for r in grid]
+    h = len(rows)
+    w = len(rows[0])
+    if any(len(r) != w for r in rows):
+        raise TswapError(TSW_EINVAL, "ragged grid rows (the reference indexes grid[y][x] for x < len(grid[0]))")
+    a = np.frombuffer("".join(rows).encode("latin-1"), dtype=np.uint8).reshape(h, w).copy()
+    return a, w, h
+
+
+def _u32p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
+class Planner:
+    """One device context (tsw_ctx) bound to a grid."""
+
+    def __init__(self, grid, device: int = 0, flags: int = 0, table_budget_bytes: int = 0):
+        self._lib = load_library()
+        cells, w, h = grid_to_bytes(grid)
+        self.w, self.h = int(w), int(h)
+        opts = _Opts(device, flags, table_budget_bytes)
+        ptr = self._lib.tsw_create(cells.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), w, h,
+                                   ctypes.byref(opts))
+        if not ptr:
+            raise TswapError(TSW_EHIP, self._lib.tsw_last_error(None).decode())
+        self._ctx = ptr
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.tsw_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc):
+        if rc != TSW_OK:
+            raise TswapError(rc, self._lib.tsw_last_error(self._ctx).decode())
+
+    # --- tswap_mapd -------------------------------------------------------
+    def plan_mapd_arrays(self, starts_xy: np.ndarray, tasks_xyxy: np.ndarray, max_t: int = 2000,
+                         trace_goals: bool = False):
+        """starts_xy: (n,2) uint32; tasks_xyxy: (m,4) uint32 (pickup x,y, delivery x,y).
+
+        Returns (rec (n, T) uint64 packed x | y<<16 | state<<32, goals (n, T) or None).
+        """
+        starts = np.ascontiguousarray(starts_xy, dtype=np.uint32).reshape(-1, 2)
+        tasks = np.ascontiguousarray(tasks_xyxy, dtype=np.uint32).reshape(-1, 4)
+        n, m = starts.shape[0], tasks.shape[0]
+        stride = max_t + 1
+        out = np.zeros((max(n, 1), stride), dtype=np.uint64)
+        T = ctypes.c_uint32(0)
+        sp = starts.ctypes.data_as(ctypes.POINTER(_Point))
+        tp = tasks.ctypes.data_as(ctypes.POINTER(_Task))
+        op = out.ctypes.data_as(ctypes.POINTER(_Rec))
+        goals = None
+        if trace_goals:
+            goals = np.zeros((max(n, 1), stride), dtype=np.uint32)
+            rc = self._lib.tsw_plan_mapd_trace(self._ctx, sp, n, tp, m, max_t, op, _u32p(goals), ctypes.byref(T))
+        else:
+            rc = self._lib.tsw_plan_mapd(self._ctx, sp, n, tp, m, max_t, op, ctypes.byref(T))
+        self._check(rc)
+        t = T.value
+        rec = out[:n, :t] & np.uint64(0xFFFFFFFFFF)
+        return rec, (goals[:n, :t] if goals is not None else None)
+
+    def tswap_mapd(self, initial_positions: Sequence, tasks: Iterable, max_t: int = 2000):
+        starts = np.array([[p[0], p[1]] for p in initial_positions], dtype=np.uint32).reshape(-1, 2)
+        tl = []
+        for t in tasks:
+            pu, dl = (t.pickup, t.delivery) if isinstance(t, Task) else (t[0], t[1])
+            tl.append([pu[0], pu[1], dl[0], dl[1]])
+        tarr = np.array(tl, dtype=np.uint32).reshape(-1, 4)
+        rec, _ = self.plan_mapd_arrays(starts, tarr, max_t)
+        x = (rec & np.uint64(0xFFFF)).astype(np.int64)
+        y = ((rec >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.int64)
+        s = ((rec >> np.uint64(32)) & np.uint64(0xFF)).astype(np.int64)
+        return [[((int(x[i, t]), int(y[i, t])), AgentState(int(s[i, t]))) for t in range(rec.shape[1])]
+                for i in range(rec.shape[0])]
+
+    # --- tswap_step (per tick, bin/centralized/manager.rs:101-144) ---------
+    def step(self, v: np.ndarray, g: np.ndarray):
+        v = np.ascontiguousarray(v, dtype=np.uint32).copy()
+        g = np.ascontiguousarray(g, dtype=np.uint32).copy()
+        if v.shape != g.shape:
+            raise TswapError(TSW_EINVAL, "v and g must have the same length")
+        self._check(self._lib.tsw_step(self._ctx, _u32p(v), _u32p(g), v.size))
+        return v, g
+
+    # --- get_path -----------------------------------------------------------
+    def get_path_next(self, start: np.ndarray, goal: np.ndarray):
+        s = np.ascontiguousarray(start, dtype=np.uint32)
+        g = np.ascontiguousarray(goal, dtype=np.uint32)
+        nxt = np.zeros(s.size, dtype=np.uint32)
+        ln = np.zeros(s.size, dtype=np.int32)
+        self._check(self._lib.tsw_get_path_next(self._ctx, _u32p(s), _u32p(g), s.size, _u32p(nxt),
+                                                ln.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return nxt, ln
+
+    # --- K1 tables ----------------------------------------------------------
+    def dist_tables(self, goals) -> np.ndarray:
+        g = np.ascontiguousarray(goals, dtype=np.uint32)
+        out = np.zeros((g.size, self.h * self.w), dtype=np.uint16)
+        self._check(self._lib.tsw_dist_tables(self._ctx, _u32p(g), g.size,
+                                              out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16))))
+        return out
+
+    def dist_tables_device(self, goals, dev_ptr: int):
+        g = np.ascontiguousarray(goals, dtype=np.uint32)
+        self._check(self._lib.tsw_dist_tables_device(self._ctx, _u32p(g), g.size, ctypes.c_void_p(dev_ptr)))
+
+    def import_tables_device(self, goals, dev_ptr: int):
+        g = np.ascontiguousarray(goals, dtype=np.uint32)
+        self._check(self._lib.tsw_import_tables_device(self._ctx, _u32p(g), g.size, ctypes.c_void_p(dev_ptr)))
+
+    def stats(self) -> dict:
+        s = Stats()
+        self._check(self._lib.tsw_get_stats(self._ctx, ctypes.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        self._check(self._lib.tsw_reset_stats(self._ctx))
+
+    def set_timing(self, on: bool):
+        self._check(self._lib.tsw_set_timing(self._ctx, 1 if on else 0))
+
+
+def tswap_mapd(grid, initial_positions, tasks, max_t: int = 2000):
+    """Drop-in for `pub fn tswap_mapd` (src/algorithm/tswap.rs:39-43)."""
+    with Planner(grid) as p:
+        return p.tswap_mapd(initial_positions, tasks, max_t)
+
+
+def tswap_step(grid, agents_v, agents_g):
+    """One `tswap_step` over cell ids (y*w+x), as the centralized manager calls it per tick."""
+    with Planner(grid) as p:
+        return p.step(np.asarray(agents_v), np.asarray(agents_g))

@@ -1,0 +1,899 @@
+// tsw_capi.hip — host runtime of the TSWAP planning core behind the C ABI
+// declared in include/tswap.h. Owns device memory, the goal-table store
+// (BFS distances + next-hop codes), the A* scratch slots and the per-step
+// orchestration of K4 (assign) -> [prequery -> K3 (A*) -> K2 (walk)]* -> record.
+//
+// Reference call structure being replaced (RenKoya1/p2p_distributed_tswap):
+//   tswap_mapd            src/algorithm/tswap.rs:39-172      -> tsw_plan_mapd
+//   tswap_step            src/algorithm/tswap.rs:174-286     -> tsw_step
+//   get_path              src/algorithm/tswap.rs:288-390     -> tsw_get_path_next
+//   plan_all_paths' step  src/bin/centralized/manager.rs:101-144 -> tsw_step
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tsw_internal.h"
+#include "tsw_launch.h"
+#include "tswap.h"
+
+using namespace tsw;
+
+namespace {
+
+thread_local std::string g_create_err;
+
+struct DevStatus {
+  WalkState ws;
+  uint32_t err;
+  uint32_t done;
+  uint32_t qcount;
+  uint32_t pad;
+};
+
+enum { CAT_BFS = 0, CAT_ASTAR = 1, CAT_WALK = 2, CAT_ASSIGN = 3, NCAT = 4 };
+
+}  // namespace
+
+struct tsw_ctx {
+  int device = 0;
+  hipStream_t s = nullptr;
+  std::string err;
+  uint32_t flags = 0;
+  DevGrid G{};
+  std::vector<uint8_t> h_nbmask;
+  uint8_t* d_nbmask = nullptr;
+  uint32_t* d_freebits = nullptr;
+  int max_lds = 65536, num_cu = 256;
+
+  // goal-table store
+  uint64_t tstride = 0;
+  uint32_t tab_cap = 0, tab_count = 0;
+  uint16_t* d_dist = nullptr;
+  uint8_t* d_nh = nullptr;
+  int32_t* d_goal_tab = nullptr;
+  std::vector<int32_t> h_goal_tab;
+  std::vector<uint32_t> h_tab_goal;
+  uint64_t table_budget = 0;
+
+  // A* scratch
+  uint32_t nslots = 0, hcap = 0;
+  uint64_t* d_heaps = nullptr;
+  uint32_t* d_gs = nullptr;
+  uint32_t* d_epochs = nullptr;
+
+  // query queue
+  AstarQuery* d_Q = nullptr;
+  size_t qcap = 0;
+  uint8_t* d_res = nullptr;
+  int32_t* d_lens = nullptr;
+  size_t rescap = 0;
+
+  DevStatus* d_stat = nullptr;
+  DevStatus* h_stat = nullptr;   // pinned, D2H
+  WalkState* h_wsinit = nullptr; // pinned, H2D
+  uint32_t chase_id = 0;
+
+  // agents
+  size_t acap = 0;
+  uint32_t *d_v = nullptr, *d_g = nullptr, *d_cnt = nullptr, *d_stamp = nullptr, *d_ap = nullptr;
+  uint8_t* d_st = nullptr;
+  int32_t *d_task = nullptr, *d_occ = nullptr;
+  // tasks
+  size_t tcap = 0;
+  uint32_t *d_pick_xy = nullptr, *d_pick = nullptr, *d_dlv = nullptr, *d_unused = nullptr;
+  uint8_t* d_used = nullptr;
+  // records
+  uint64_t* d_rec = nullptr;
+  size_t rec_cap = 0;
+  uint32_t* d_grec = nullptr;
+  size_t grec_cap = 0;
+  // temporaries
+  uint32_t *d_tmp_a = nullptr, *d_tmp_b = nullptr;
+  size_t tmp_cap = 0;
+
+  // stats / timing
+  tsw_stats st{};
+  bool timing = true;
+  struct Ev {
+    int cat;
+    hipEvent_t a, b;
+  };
+  std::vector<Ev> pending;
+  std::vector<hipEvent_t> pool;
+};
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess) {                                                           \
+      c->err = std::string(#expr) + " failed: " + hipGetErrorString(e_);             \
+      return TSW_EHIP;                                                                \
+    }                                                                                 \
+  } while (0)
+
+#define RET(code, msg)   \
+  do {                   \
+    c->err = (msg);      \
+    return (code);       \
+  } while (0)
+
+#define TRY(expr)            \
+  do {                       \
+    int r_ = (expr);         \
+    if (r_ != TSW_OK) return r_; \
+  } while (0)
+
+namespace {
+
+template <class T>
+hipError_t dgrow(T*& p, size_t& cap, size_t need, bool zero = false) {
+  if (need <= cap && p) return hipSuccess;
+  if (p) {
+    hipError_t e = hipFree(p);
+    if (e != hipSuccess) return e;
+  }
+  p = nullptr;
+  size_t nc = std::max<size_t>(need, std::max<size_t>(cap + cap / 2, 16));
+  hipError_t e = hipMalloc(&p, nc * sizeof(T));
+  if (e != hipSuccess) {
+    cap = 0;
+    p = nullptr;
+    return e;
+  }
+  cap = nc;
+  if (zero) return hipMemset(p, 0, nc * sizeof(T));
+  return hipSuccess;
+}
+
+hipEvent_t ev_get(tsw_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+struct Timer {
+  tsw_ctx* c;
+  int cat;
+  hipEvent_t a = nullptr, b = nullptr;
+  Timer(tsw_ctx* c_, int cat_) : c(c_), cat(cat_) {
+    if (c->timing) {
+      a = ev_get(c);
+      b = ev_get(c);
+      hipEventRecord(a, c->s);
+    }
+  }
+  ~Timer() {
+    if (a) {
+      hipEventRecord(b, c->s);
+      c->pending.push_back({cat, a, b});
+    }
+  }
+};
+
+void resolve_timing(tsw_ctx* c) {
+  if (c->pending.empty()) return;
+  hipEventSynchronize(c->pending.back().b);
+  for (auto& e : c->pending) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e.a, e.b);
+    switch (e.cat) {
+      case CAT_BFS: c->st.bfs_ms += ms; break;
+      case CAT_ASTAR: c->st.astar_ms += ms; break;
+      case CAT_WALK: c->st.walker_ms += ms; break;
+      case CAT_ASSIGN: c->st.assign_ms += ms; break;
+    }
+    c->pool.push_back(e.a);
+    c->pool.push_back(e.b);
+  }
+  c->pending.clear();
+}
+
+int set_device(tsw_ctx* c) {
+  HIPCHK(hipSetDevice(c->device));
+  return TSW_OK;
+}
+
+bool cell_ok(const tsw_ctx* c, uint32_t x, uint32_t y, uint32_t* cell) {
+  if (x >= c->G.W || y >= c->G.H) return false;
+  const uint32_t cc = y * c->G.W + x;
+  if (!(c->h_nbmask[cc] & NB_FREE)) return false;
+  *cell = cc;
+  return true;
+}
+
+bool cell_id_ok(const tsw_ctx* c, uint32_t cell) {
+  return cell < c->G.ncell && (c->h_nbmask[cell] & NB_FREE);
+}
+
+int ensure_tmp(tsw_ctx* c, size_t k) {
+  if (k <= c->tmp_cap && c->d_tmp_a) return TSW_OK;
+  size_t ca = c->tmp_cap, cb = c->tmp_cap;
+  HIPCHK(hipStreamSynchronize(c->s));
+  HIPCHK(dgrow(c->d_tmp_a, ca, k));
+  HIPCHK(dgrow(c->d_tmp_b, cb, k));
+  c->tmp_cap = std::min(ca, cb);
+  return TSW_OK;
+}
+
+int ensure_astar_scratch(tsw_ctx* c) {
+  if (c->d_heaps) return TSW_OK;
+  const uint64_t ncell = c->G.ncell;
+  c->hcap = (uint32_t)std::min<uint64_t>(4ull * ncell + 8ull, 1ull << 16);
+  const uint64_t per_slot = (uint64_t)c->hcap * 8ull + ncell * 4ull;
+  const uint64_t budget = 4ull << 30;
+  uint64_t ns = budget / per_slot;
+  ns = std::max<uint64_t>(64, std::min<uint64_t>(ns, 16384));
+  c->nslots = (uint32_t)ns;
+  HIPCHK(hipMalloc(&c->d_heaps, (size_t)ns * c->hcap * 8ull));
+  HIPCHK(hipMalloc(&c->d_gs, (size_t)ns * ncell * 4ull));
+  HIPCHK(hipMemset(c->d_gs, 0, (size_t)ns * ncell * 4ull));
+  HIPCHK(hipMalloc(&c->d_epochs, (size_t)ns * 4ull));
+  HIPCHK(hipMemset(c->d_epochs, 0, (size_t)ns * 4ull));
+  return TSW_OK;
+}
+
+int ensure_queue(tsw_ctx* c, size_t need) {
+  if (need <= c->qcap && c->d_Q) return TSW_OK;
+  HIPCHK(hipStreamSynchronize(c->s));
+  HIPCHK(dgrow(c->d_Q, c->qcap, need));
+  return TSW_OK;
+}
+
+int ensure_res(tsw_ctx* c, size_t need) {
+  if (need <= c->rescap && c->d_res) return TSW_OK;
+  HIPCHK(hipStreamSynchronize(c->s));
+  size_t a = c->rescap, b = c->rescap;
+  HIPCHK(dgrow(c->d_res, a, need));
+  HIPCHK(dgrow(c->d_lens, b, need));
+  c->rescap = std::min(a, b);
+  return TSW_OK;
+}
+
+int check_err(tsw_ctx* c) {
+  uint32_t e = 0;
+  HIPCHK(hipMemcpyAsync(&c->h_stat->err, &c->d_stat->err, 4, hipMemcpyDeviceToHost, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  e = c->h_stat->err;
+  if (e) {
+    char buf[160];
+    snprintf(buf, sizeof buf, "device error bits 0x%x (1 heap overflow, 2 dist overflow, 4 g overflow, 8 no table)",
+             e);
+    c->err = buf;
+    HIPCHK(hipMemsetAsync(&c->d_stat->err, 0, 4, c->s));
+    return (e & (ERR_HEAP_OVERFLOW | ERR_DIST_OVERFLOW | ERR_G_OVERFLOW)) ? TSW_EOVERFLOW : TSW_EINVAL;
+  }
+  return TSW_OK;
+}
+
+// Run K3 over the queued queries until none are left (eager next hops).
+int resolve_all_unknown(tsw_ctx* c, const std::vector<uint32_t>& goals, const std::vector<uint32_t>& slots) {
+  if (goals.empty()) return TSW_OK;
+  TRY(ensure_astar_scratch(c));
+  TRY(ensure_tmp(c, goals.size()));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_a, goals.data(), goals.size() * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
+  TRY(ensure_queue(c, std::max<size_t>(c->qcap, 1u << 16)));
+  for (int iter = 0; iter < 1000000; ++iter) {
+    HIPCHK(hipMemsetAsync(&c->d_stat->qcount, 0, 4, c->s));
+    HIPCHK(launch_enqueue_unknown(c->G, c->d_tmp_a, c->d_tmp_b, (uint32_t)goals.size(), c->d_nh, c->tstride,
+                                  c->d_Q, &c->d_stat->qcount, (uint32_t)c->qcap, c->s));
+    HIPCHK(hipMemcpyAsync(&c->h_stat->qcount, &c->d_stat->qcount, 4, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    const uint32_t cnt = c->h_stat->qcount;
+    if (cnt == 0) break;
+    const uint32_t run = (uint32_t)std::min<size_t>(cnt, c->qcap);
+    {
+      Timer t(c, CAT_ASTAR);
+      HIPCHK(launch_astar(c->G, c->d_Q, nullptr, run, run, c->d_nh, c->tstride, nullptr, nullptr, c->d_heaps,
+                          c->hcap, c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
+    }
+    c->st.astar_queries += run;
+    c->st.astar_launches++;
+    TRY(check_err(c));
+    if (cnt <= c->qcap) break;
+  }
+  return TSW_OK;
+}
+
+bool eager_policy(const tsw_ctx* c, size_t new_tables) {
+  if (c->flags & TSW_F_LAZY_NEXTHOP) return false;
+  if (c->flags & TSW_F_EAGER_NEXTHOP) return true;
+  return c->G.ncell <= 4096 && (uint64_t)new_tables * c->G.ncell <= (8ull << 20);
+}
+
+// Make sure every goal in `goals` (valid free cells) has a table.
+int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
+  std::vector<uint32_t> newg;
+  newg.reserve(goals_in.size());
+  for (uint32_t g : goals_in)
+    if (c->h_goal_tab[g] < 0) {
+      c->h_goal_tab[g] = -2;  // mark (dedupe)
+      newg.push_back(g);
+    }
+  if (newg.empty()) return TSW_OK;
+  const size_t need = (size_t)c->tab_count + newg.size();
+  const uint64_t per_tab = c->tstride * 3ull;
+  if (need > c->tab_cap) {
+    size_t nc = std::max<size_t>(need, std::max<size_t>((size_t)c->tab_cap * 2, 64));
+    const uint64_t max_tabs = c->table_budget / per_tab;
+    if (nc > max_tabs) nc = std::max<size_t>(need, (size_t)max_tabs);
+    if ((uint64_t)need > max_tabs) {
+      for (uint32_t g : newg) c->h_goal_tab[g] = -1;
+      RET(TSW_ENOMEM, "goal-table budget exceeded (raise tsw_opts.table_budget_bytes)");
+    }
+    HIPCHK(hipStreamSynchronize(c->s));
+    uint16_t* nd = nullptr;
+    uint8_t* nn = nullptr;
+    HIPCHK(hipMalloc(&nd, nc * c->tstride * 2ull));
+    HIPCHK(hipMalloc(&nn, nc * c->tstride));
+    if (c->tab_count) {
+      HIPCHK(hipMemcpyAsync(nd, c->d_dist, (size_t)c->tab_count * c->tstride * 2ull, hipMemcpyDeviceToDevice, c->s));
+      HIPCHK(hipMemcpyAsync(nn, c->d_nh, (size_t)c->tab_count * c->tstride, hipMemcpyDeviceToDevice, c->s));
+      HIPCHK(hipStreamSynchronize(c->s));
+    }
+    if (c->d_dist) HIPCHK(hipFree(c->d_dist));
+    if (c->d_nh) HIPCHK(hipFree(c->d_nh));
+    c->d_dist = nd;
+    c->d_nh = nn;
+    c->tab_cap = (uint32_t)nc;
+    c->h_tab_goal.resize(nc, 0);
+  }
+  std::vector<uint32_t> slots(newg.size());
+  for (size_t k = 0; k < newg.size(); ++k) {
+    slots[k] = c->tab_count + (uint32_t)k;
+    c->h_goal_tab[newg[k]] = (int32_t)slots[k];
+    c->h_tab_goal[slots[k]] = newg[k];
+  }
+  c->tab_count = (uint32_t)need;
+  TRY(ensure_tmp(c, newg.size()));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_a, newg.data(), newg.size() * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
+  {
+    Timer t(c, CAT_BFS);
+    HIPCHK(launch_bfs(c->G, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh,
+                      c->tstride, &c->d_stat->err, c->max_lds, c->num_cu, c->s));
+  }
+  c->st.bfs_goals += newg.size();
+  c->st.bfs_launches++;
+  HIPCHK(hipMemcpyAsync(c->d_goal_tab, c->h_goal_tab.data(), (size_t)c->G.ncell * 4, hipMemcpyHostToDevice, c->s));
+  TRY(check_err(c));
+  c->st.tables = c->tab_count;
+  if (eager_policy(c, newg.size())) TRY(resolve_all_unknown(c, newg, slots));
+  return TSW_OK;
+}
+
+int ensure_agents(tsw_ctx* c, size_t n) {
+  if (n <= c->acap && c->d_v) return TSW_OK;
+  HIPCHK(hipStreamSynchronize(c->s));
+  size_t cap = std::max<size_t>(n, 64);
+  auto fre = [](void* p) {
+    if (p) (void)hipFree(p);
+  };
+  fre(c->d_v); fre(c->d_g); fre(c->d_stamp); fre(c->d_ap); fre(c->d_st); fre(c->d_task);
+  HIPCHK(hipMalloc(&c->d_v, cap * 4));
+  HIPCHK(hipMalloc(&c->d_g, cap * 4));
+  HIPCHK(hipMalloc(&c->d_stamp, cap * 4));
+  HIPCHK(hipMemset(c->d_stamp, 0, cap * 4));
+  HIPCHK(hipMalloc(&c->d_ap, (cap + 1) * 4));
+  HIPCHK(hipMalloc(&c->d_st, cap));
+  HIPCHK(hipMalloc(&c->d_task, cap * 4));
+  if (!c->d_occ) {
+    HIPCHK(hipMalloc(&c->d_occ, (size_t)c->G.ncell * 4));
+    HIPCHK(hipMalloc(&c->d_cnt, (size_t)c->G.ncell * 4));
+  }
+  c->acap = cap;
+  c->chase_id = 0;
+  return TSW_OK;
+}
+
+AgentsDev agents_dev(tsw_ctx* c, uint32_t n) {
+  AgentsDev A;
+  A.n = n;
+  A.v = c->d_v;
+  A.g = c->d_g;
+  A.st = c->d_st;
+  A.task = c->d_task;
+  A.occ = c->d_occ;
+  A.cnt = c->d_cnt;
+  A.stamp = c->d_stamp;
+  A.ap = c->d_ap;
+  return A;
+}
+
+// One tswap_step: [prequery -> K3 -> K2]* until the walker finishes both phases.
+int run_step_rounds(tsw_ctx* c, const AgentsDev& A) {
+  WalkState ws{};
+  ws.chase_id = c->chase_id;
+  *c->h_wsinit = ws;
+  HIPCHK(hipMemcpyAsync(&c->d_stat->ws, c->h_wsinit, sizeof(WalkState), hipMemcpyHostToDevice, c->s));
+  TRY(ensure_queue(c, std::max<size_t>(A.n, 64)));
+  TRY(ensure_astar_scratch(c));
+  const uint64_t max_rounds = 4ull * A.n + 16;
+  for (uint64_t round = 0;; ++round) {
+    if (round > max_rounds) RET(TSW_EINVAL, "walker made no progress");
+    HIPCHK(hipMemsetAsync(&c->d_stat->qcount, 0, 4, c->s));
+    HIPCHK(launch_prequery(A, c->d_goal_tab, c->d_nh, c->tstride, c->d_Q, &c->d_stat->qcount, &c->d_stat->err,
+                           c->s));
+    {
+      Timer t(c, CAT_ASTAR);
+      HIPCHK(launch_astar(c->G, c->d_Q, &c->d_stat->qcount, 0, A.n, c->d_nh, c->tstride, nullptr, nullptr,
+                          c->d_heaps, c->hcap, c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
+    }
+    c->st.astar_launches++;
+    {
+      Timer t(c, CAT_WALK);
+      HIPCHK(launch_walk(A, c->d_goal_tab, c->d_nh, c->tstride, c->G.W, &c->d_stat->ws, &c->d_stat->err, c->s));
+    }
+    c->st.walker_launches++;
+    HIPCHK(hipMemcpyAsync(c->h_stat, c->d_stat, sizeof(DevStatus), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    c->st.astar_queries += c->h_stat->qcount;
+    if (c->h_stat->err) TRY(check_err(c));
+    if (c->h_stat->ws.phase == 2) {
+      c->chase_id = c->h_stat->ws.chase_id;
+      return TSW_OK;
+    }
+  }
+}
+
+int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* tasks, uint32_t m,
+              uint32_t max_t, tsw_rec* out, uint32_t* goal_out, uint32_t* out_T) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!out_T || (n && (!starts || !out)) || (m && !tasks)) RET(TSW_EINVAL, "null argument");
+  if (max_t > (1u << 20)) RET(TSW_EINVAL, "max_t too large");
+  TRY(set_device(c));
+  std::vector<uint32_t> vcell(n), pick(m), dlv(m), pick_xy(m);
+  std::vector<uint32_t> goalset;
+  goalset.reserve(n + 2 * (size_t)m);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!cell_ok(c, starts[i].x, starts[i].y, &vcell[i]))
+      RET(TSW_EINVAL, "start position off-grid or blocked (reference panics at tswap.rs:94)");
+    goalset.push_back(vcell[i]);
+  }
+  for (uint32_t k = 0; k < m; ++k) {
+    if (!cell_ok(c, tasks[k].pickup.x, tasks[k].pickup.y, &pick[k]))
+      RET(TSW_EINVAL, "task pickup off-grid or blocked (reference panics at tswap.rs:136)");
+    if (!cell_ok(c, tasks[k].delivery.x, tasks[k].delivery.y, &dlv[k]))
+      RET(TSW_EINVAL, "task delivery off-grid or blocked (reference panics at tswap.rs:112)");
+    pick_xy[k] = tasks[k].pickup.x | (tasks[k].pickup.y << 16);
+    goalset.push_back(pick[k]);
+    goalset.push_back(dlv[k]);
+  }
+  TRY(ensure_agents(c, std::max<uint32_t>(n, 1)));
+  if (m > c->tcap || !c->d_used) {
+    HIPCHK(hipStreamSynchronize(c->s));
+    size_t a = c->tcap, b = c->tcap, d = c->tcap, e = c->tcap;
+    HIPCHK(dgrow(c->d_pick_xy, a, std::max<uint32_t>(m, 1)));
+    HIPCHK(dgrow(c->d_pick, b, std::max<uint32_t>(m, 1)));
+    HIPCHK(dgrow(c->d_dlv, d, std::max<uint32_t>(m, 1)));
+    HIPCHK(dgrow(c->d_used, e, std::max<uint32_t>(m, 1)));
+    c->tcap = std::min(std::min(a, b), std::min(d, e));
+    if (!c->d_unused) HIPCHK(hipMalloc(&c->d_unused, 4));
+  }
+  const size_t stride_t = (size_t)max_t + 1;
+  const size_t recs = stride_t * std::max<uint32_t>(n, 1);
+  if (recs > c->rec_cap || !c->d_rec) {
+    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(dgrow(c->d_rec, c->rec_cap, recs));
+  }
+  if (goal_out && (recs > c->grec_cap || !c->d_grec)) {
+    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(dgrow(c->d_grec, c->grec_cap, recs));
+  }
+  // agent + task state
+  if (n) {
+    HIPCHK(hipMemcpyAsync(c->d_v, vcell.data(), n * 4ull, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_g, vcell.data(), n * 4ull, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemsetAsync(c->d_st, 0, n, c->s));
+    HIPCHK(hipMemsetAsync(c->d_task, 0xFF, n * 4ull, c->s));
+  }
+  if (m) {
+    HIPCHK(hipMemcpyAsync(c->d_pick_xy, pick_xy.data(), m * 4ull, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_pick, pick.data(), m * 4ull, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_dlv, dlv.data(), m * 4ull, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemsetAsync(c->d_used, 0, m, c->s));
+  }
+  HIPCHK(hipMemcpyAsync(c->d_unused, &m, 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));  // host vectors above go out of scope only at return, but keep it simple
+  AgentsDev A = agents_dev(c, n);
+  TasksDev TK;
+  TK.m = m;
+  TK.pick_xy = c->d_pick_xy;
+  TK.pick = c->d_pick;
+  TK.dlv = c->d_dlv;
+  TK.used = c->d_used;
+  TK.unused = c->d_unused;
+  HIPCHK(launch_occ_build(A, c->G.ncell, c->s));
+  TRY(ensure_tables(c, goalset));
+
+  uint32_t t = 0;
+  for (;;) {
+    {
+      Timer tm(c, CAT_ASSIGN);
+      HIPCHK(launch_assign(A, TK, c->G.W, &c->d_stat->done, c->s));
+    }
+    c->st.assign_launches++;
+    if (n) TRY(run_step_rounds(c, A));
+    else {
+      HIPCHK(hipMemcpyAsync(c->h_stat, c->d_stat, sizeof(DevStatus), hipMemcpyDeviceToHost, c->s));
+      HIPCHK(hipStreamSynchronize(c->s));
+    }
+    HIPCHK(launch_record(A, c->G.W, c->d_rec + (size_t)t * n, goal_out ? c->d_grec + (size_t)t * n : nullptr,
+                         c->s));
+    ++t;
+    c->st.steps++;
+    if (c->h_stat->done || t > max_t) break;
+  }
+  *out_T = t;
+  if (n) {
+    std::vector<uint64_t> rec((size_t)t * n);
+    HIPCHK(hipMemcpyAsync(rec.data(), c->d_rec, rec.size() * 8, hipMemcpyDeviceToHost, c->s));
+    std::vector<uint32_t> grec;
+    if (goal_out) {
+      grec.resize((size_t)t * n);
+      HIPCHK(hipMemcpyAsync(grec.data(), c->d_grec, grec.size() * 4, hipMemcpyDeviceToHost, c->s));
+    }
+    HIPCHK(hipStreamSynchronize(c->s));
+    for (uint32_t tt = 0; tt < t; ++tt)
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t r = rec[(size_t)tt * n + i];
+        tsw_rec& o = out[(size_t)i * stride_t + tt];
+        o.x = (uint16_t)(r & 0xFFFF);
+        o.y = (uint16_t)((r >> 16) & 0xFFFF);
+        o.state = (uint8_t)((r >> 32) & 0xFF);
+        o.pad[0] = o.pad[1] = o.pad[2] = 0;
+        if (goal_out) goal_out[(size_t)i * stride_t + tt] = grec[(size_t)tt * n + i];
+      }
+  }
+  resolve_timing(c);
+  c->st.plan_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return TSW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts* opts) {
+  if (!cells || w == 0 || h == 0) {
+    g_create_err = "tsw_create: empty grid";
+    return nullptr;
+  }
+  if (w > MAX_WH || h > MAX_WH || (uint64_t)w * h > MAX_CELLS) {
+    g_create_err = "tsw_create: grid exceeds 2048 per side or 2^20 cells";
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    g_create_err = "tsw_create: no HIP device visible (the HIP path has no CPU fallback)";
+    return nullptr;
+  }
+  tsw_ctx* c = new tsw_ctx();
+  c->device = opts ? opts->device : 0;
+  c->flags = opts ? opts->flags : 0;
+  if (c->device < 0 || c->device >= ndev) {
+    g_create_err = "tsw_create: bad device ordinal";
+    delete c;
+    return nullptr;
+  }
+  auto fail = [&](const char* what, hipError_t e) {
+    g_create_err = std::string("tsw_create: ") + what + ": " + hipGetErrorString(e);
+    tsw_destroy(c);
+    return (tsw_ctx*)nullptr;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(c->device)) != hipSuccess) return fail("hipSetDevice", e);
+  if ((e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking)) != hipSuccess) return fail("stream", e);
+  hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, c->device);
+  hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, c->device);
+  if (c->max_lds <= 0) c->max_lds = 65536;
+  if (c->num_cu <= 0) c->num_cu = 256;
+
+  const uint32_t ncell = w * h, ncp = (ncell + 7u) & ~7u, Ww = (w + 31u) / 32u;
+  c->G.W = w;
+  c->G.H = h;
+  c->G.ncell = ncell;
+  c->G.Ww = Ww;
+  c->tstride = ncp;
+  // graph build (tswap.rs:44-77): '@' blocked, neighbours S,E,N,W
+  c->h_nbmask.assign(ncp, 0);
+  std::vector<uint32_t> fb((size_t)h * Ww, 0u);
+  for (uint32_t y = 0; y < h; ++y)
+    for (uint32_t x = 0; x < w; ++x)
+      if (cells[(size_t)y * w + x] != '@') {
+        c->h_nbmask[(size_t)y * w + x] = NB_FREE;
+        fb[(size_t)y * Ww + (x >> 5)] |= 1u << (x & 31u);
+      }
+  auto is_free = [&](long x, long y) {
+    return x >= 0 && y >= 0 && x < (long)w && y < (long)h && cells[(size_t)y * w + x] != '@';
+  };
+  for (uint32_t y = 0; y < h; ++y)
+    for (uint32_t x = 0; x < w; ++x) {
+      uint8_t& m = c->h_nbmask[(size_t)y * w + x];
+      if (!(m & NB_FREE)) continue;
+      if (is_free(x, (long)y + 1)) m |= 1;
+      if (is_free((long)x + 1, y)) m |= 2;
+      if (is_free(x, (long)y - 1)) m |= 4;
+      if (is_free((long)x - 1, y)) m |= 8;
+    }
+  if ((e = hipMalloc(&c->d_nbmask, ncp)) != hipSuccess) return fail("malloc nbmask", e);
+  if ((e = hipMemcpy(c->d_nbmask, c->h_nbmask.data(), ncp, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail("copy nbmask", e);
+  if ((e = hipMalloc(&c->d_freebits, fb.size() * 4)) != hipSuccess) return fail("malloc freebits", e);
+  if ((e = hipMemcpy(c->d_freebits, fb.data(), fb.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail("copy freebits", e);
+  c->G.nbmask = c->d_nbmask;
+  c->G.freebits = c->d_freebits;
+  c->h_goal_tab.assign(ncell, -1);
+  if ((e = hipMalloc(&c->d_goal_tab, (size_t)ncell * 4)) != hipSuccess) return fail("malloc goal_tab", e);
+  if ((e = hipMemcpy(c->d_goal_tab, c->h_goal_tab.data(), (size_t)ncell * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail("copy goal_tab", e);
+  if ((e = hipMalloc(&c->d_stat, sizeof(DevStatus))) != hipSuccess) return fail("malloc status", e);
+  if ((e = hipMemset(c->d_stat, 0, sizeof(DevStatus))) != hipSuccess) return fail("memset status", e);
+  if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
+    return fail("pinned status", e);
+  if ((e = hipHostMalloc(&c->h_wsinit, sizeof(WalkState), hipHostMallocDefault)) != hipSuccess)
+    return fail("pinned ws", e);
+  memset(c->h_stat, 0, sizeof(DevStatus));
+  size_t freeb = 0, totalb = 0;
+  hipMemGetInfo(&freeb, &totalb);
+  c->table_budget = (opts && opts->table_budget_bytes) ? opts->table_budget_bytes : (uint64_t)(freeb / 2);
+  return c;
+}
+
+void tsw_destroy(tsw_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->s) hipStreamSynchronize(c->s);
+  auto fre = [](void* p) {
+    if (p) (void)hipFree(p);
+  };
+  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
+  fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
+  fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_stamp); fre(c->d_ap); fre(c->d_st);
+  fre(c->d_task); fre(c->d_occ); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
+  fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
+  if (c->h_stat) hipHostFree(c->h_stat);
+  if (c->h_wsinit) hipHostFree(c->h_wsinit);
+  for (auto& e : c->pending) {
+    hipEventDestroy(e.a);
+    hipEventDestroy(e.b);
+  }
+  for (auto e : c->pool) hipEventDestroy(e);
+  if (c->s) hipStreamDestroy(c->s);
+  delete c;
+}
+
+const char* tsw_last_error(const tsw_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
+
+int tsw_plan_mapd(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* tasks, uint32_t m,
+                  uint32_t max_t, tsw_rec* out, uint32_t* out_T) {
+  if (!c) return TSW_EINVAL;
+  return plan_impl(c, starts, n, tasks, m, max_t, out, nullptr, out_T);
+}
+
+int tsw_plan_mapd_trace(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* tasks, uint32_t m,
+                        uint32_t max_t, tsw_rec* out, uint32_t* goal_out, uint32_t* out_T) {
+  if (!c) return TSW_EINVAL;
+  return plan_impl(c, starts, n, tasks, m, max_t, out, goal_out, out_T);
+}
+
+int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
+  if (!c) return TSW_EINVAL;
+  if (n == 0) return TSW_OK;
+  if (!v || !g) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  std::vector<uint32_t> goals;
+  goals.reserve(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!cell_id_ok(c, v[i]) || !cell_id_ok(c, g[i])) RET(TSW_EINVAL, "agent cell off-grid or blocked");
+    goals.push_back(g[i]);
+  }
+  TRY(ensure_agents(c, n));
+  HIPCHK(hipMemcpyAsync(c->d_v, v, n * 4ull, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_g, g, n * 4ull, hipMemcpyHostToDevice, c->s));
+  AgentsDev A = agents_dev(c, n);
+  HIPCHK(launch_occ_build(A, c->G.ncell, c->s));
+  TRY(ensure_tables(c, goals));
+  TRY(run_step_rounds(c, A));
+  HIPCHK(hipMemcpyAsync(v, c->d_v, n * 4ull, hipMemcpyDeviceToHost, c->s));
+  HIPCHK(hipMemcpyAsync(g, c->d_g, n * 4ull, hipMemcpyDeviceToHost, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  c->st.steps++;
+  resolve_timing(c);
+  return TSW_OK;
+}
+
+int tsw_get_path_next(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, uint32_t k, uint32_t* next,
+                      int32_t* len) {
+  if (!c) return TSW_EINVAL;
+  if (k == 0) return TSW_OK;
+  if (!start || !goal || !next || !len) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  std::vector<AstarQuery> q;
+  q.reserve(k);
+  for (uint32_t i = 0; i < k; ++i) {
+    if (!cell_id_ok(c, start[i]) || !cell_id_ok(c, goal[i])) RET(TSW_EINVAL, "query cell off-grid or blocked");
+    if (start[i] == goal[i]) {
+      next[i] = start[i];
+      len[i] = 1;
+      continue;
+    }
+    AstarQuery a;
+    a.v = start[i];
+    a.goal = goal[i];
+    a.tab = -1;
+    a.out = i;
+    q.push_back(a);
+  }
+  if (q.empty()) return TSW_OK;
+  TRY(ensure_astar_scratch(c));
+  TRY(ensure_queue(c, q.size()));
+  TRY(ensure_res(c, k));
+  HIPCHK(hipMemcpyAsync(c->d_Q, q.data(), q.size() * sizeof(AstarQuery), hipMemcpyHostToDevice, c->s));
+  {
+    Timer t(c, CAT_ASTAR);
+    HIPCHK(launch_astar(c->G, c->d_Q, nullptr, (uint32_t)q.size(), (uint32_t)q.size(), nullptr, 0, c->d_res,
+                        c->d_lens, c->d_heaps, c->hcap, c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
+  }
+  c->st.astar_queries += q.size();
+  c->st.astar_launches++;
+  std::vector<uint8_t> res(k);
+  std::vector<int32_t> lens(k);
+  HIPCHK(hipMemcpyAsync(res.data(), c->d_res, k, hipMemcpyDeviceToHost, c->s));
+  HIPCHK(hipMemcpyAsync(lens.data(), c->d_lens, k * 4ull, hipMemcpyDeviceToHost, c->s));
+  TRY(check_err(c));
+  for (const auto& a : q) {
+    const uint8_t code = res[a.out];
+    uint32_t nx = a.v;
+    switch (code) {
+      case 0: nx = a.v + c->G.W; break;
+      case 1: nx = a.v + 1; break;
+      case 2: nx = a.v - c->G.W; break;
+      case 3: nx = a.v - 1; break;
+      default: nx = a.v; break;
+    }
+    next[a.out] = nx;
+    len[a.out] = lens[a.out];
+  }
+  resolve_timing(c);
+  return TSW_OK;
+}
+
+int tsw_dist_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16_t* out) {
+  if (!c) return TSW_EINVAL;
+  if (k == 0) return TSW_OK;
+  if (!goals || !out) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  std::vector<uint32_t> gv(goals, goals + k);
+  for (uint32_t g : gv)
+    if (!cell_id_ok(c, g)) RET(TSW_EINVAL, "goal cell off-grid or blocked");
+  TRY(ensure_tables(c, gv));
+  const size_t ncell = c->G.ncell;
+  for (uint32_t i = 0; i < k; ++i) {
+    const int32_t slot = c->h_goal_tab[gv[i]];
+    HIPCHK(hipMemcpyAsync(out + (size_t)i * ncell, c->d_dist + (size_t)slot * c->tstride, ncell * 2,
+                          hipMemcpyDeviceToHost, c->s));
+  }
+  HIPCHK(hipStreamSynchronize(c->s));
+  resolve_timing(c);
+  return TSW_OK;
+}
+
+int tsw_dist_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16_t* dev_out) {
+  if (!c) return TSW_EINVAL;
+  if (k == 0) return TSW_OK;
+  if (!goals || !dev_out) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  for (uint32_t i = 0; i < k; ++i)
+    if (!cell_id_ok(c, goals[i])) RET(TSW_EINVAL, "goal cell off-grid or blocked");
+  TRY(ensure_tmp(c, k));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_a, goals, (size_t)k * 4, hipMemcpyHostToDevice, c->s));
+  {
+    Timer t(c, CAT_BFS);
+    HIPCHK(launch_bfs(c->G, c->d_tmp_a, nullptr, k, dev_out, c->G.ncell, nullptr, 0, &c->d_stat->err, c->max_lds,
+                      c->num_cu, c->s));
+  }
+  c->st.bfs_goals += k;
+  c->st.bfs_launches++;
+  TRY(check_err(c));
+  resolve_timing(c);
+  return TSW_OK;
+}
+
+int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, const uint16_t* dev_tables) {
+  if (!c) return TSW_EINVAL;
+  if (k == 0) return TSW_OK;
+  if (!goals || !dev_tables) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  std::vector<uint32_t> newg, src;
+  for (uint32_t i = 0; i < k; ++i) {
+    if (!cell_id_ok(c, goals[i])) RET(TSW_EINVAL, "goal cell off-grid or blocked");
+    if (c->h_goal_tab[goals[i]] < 0) {
+      c->h_goal_tab[goals[i]] = -2;
+      newg.push_back(goals[i]);
+      src.push_back(i);
+    }
+  }
+  for (uint32_t g : newg) c->h_goal_tab[g] = -1;
+  if (newg.empty()) return TSW_OK;
+  const size_t need = (size_t)c->tab_count + newg.size();
+  if (need > c->tab_cap) {
+    // grow through ensure_tables' path by temporarily computing nothing: reuse its allocator
+    const uint64_t per_tab = c->tstride * 3ull;
+    size_t nc = std::max<size_t>(need, std::max<size_t>((size_t)c->tab_cap * 2, 64));
+    const uint64_t max_tabs = c->table_budget / per_tab;
+    if ((uint64_t)need > max_tabs) RET(TSW_ENOMEM, "goal-table budget exceeded");
+    nc = std::min<size_t>(nc, (size_t)max_tabs);
+    HIPCHK(hipStreamSynchronize(c->s));
+    uint16_t* nd = nullptr;
+    uint8_t* nn = nullptr;
+    HIPCHK(hipMalloc(&nd, nc * c->tstride * 2ull));
+    HIPCHK(hipMalloc(&nn, nc * c->tstride));
+    if (c->tab_count) {
+      HIPCHK(hipMemcpyAsync(nd, c->d_dist, (size_t)c->tab_count * c->tstride * 2ull, hipMemcpyDeviceToDevice, c->s));
+      HIPCHK(hipMemcpyAsync(nn, c->d_nh, (size_t)c->tab_count * c->tstride, hipMemcpyDeviceToDevice, c->s));
+      HIPCHK(hipStreamSynchronize(c->s));
+    }
+    if (c->d_dist) HIPCHK(hipFree(c->d_dist));
+    if (c->d_nh) HIPCHK(hipFree(c->d_nh));
+    c->d_dist = nd;
+    c->d_nh = nn;
+    c->tab_cap = (uint32_t)nc;
+    c->h_tab_goal.resize(nc, 0);
+  }
+  std::vector<uint32_t> slots(newg.size());
+  const size_t ncell = c->G.ncell;
+  for (size_t j = 0; j < newg.size(); ++j) {
+    slots[j] = c->tab_count + (uint32_t)j;
+    c->h_goal_tab[newg[j]] = (int32_t)slots[j];
+    c->h_tab_goal[slots[j]] = newg[j];
+    HIPCHK(hipMemcpyAsync(c->d_dist + (size_t)slots[j] * c->tstride, dev_tables + (size_t)src[j] * ncell, ncell * 2,
+                          hipMemcpyDeviceToDevice, c->s));
+  }
+  c->tab_count = (uint32_t)need;
+  TRY(ensure_tmp(c, newg.size()));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_a, newg.data(), newg.size() * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(launch_classify(c->G, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_goal_tab, c->h_goal_tab.data(), ncell * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  c->st.tables = c->tab_count;
+  if (eager_policy(c, newg.size())) TRY(resolve_all_unknown(c, newg, slots));
+  return TSW_OK;
+}
+
+int tsw_get_stats(const tsw_ctx* c, tsw_stats* out) {
+  if (!c || !out) return TSW_EINVAL;
+  resolve_timing(const_cast<tsw_ctx*>(c));
+  *out = c->st;
+  return TSW_OK;
+}
+
+int tsw_reset_stats(tsw_ctx* c) {
+  if (!c) return TSW_EINVAL;
+  resolve_timing(c);
+  const uint64_t tabs = c->st.tables;
+  c->st = tsw_stats{};
+  c->st.tables = tabs;
+  return TSW_OK;
+}
+
+int tsw_set_timing(tsw_ctx* c, int enabled) {
+  if (!c) return TSW_EINVAL;
+  resolve_timing(c);
+  c->timing = enabled != 0;
+  return TSW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,850 @@
+// tsw_kernels.hip — gfx950 kernels of the TSWAP planning core.
+//
+//   K1 k_bfs        batched per-goal BFS distance tables (bit-parallel rows,
+//                   LDS-resident frontier/visited bitmaps and u16 table,
+//                   one coalesced 16-B-per-lane write-out) fused with the
+//                   next-hop classification of every cell (unique optimal
+//                   neighbour / unreachable fallback / needs-A*).
+//   K3 k_astar      exact get_path() next hop (tswap.rs:288-390): one query
+//                   per lane, Rust std BinaryHeap sift semantics restated.
+//   K2 k_walk       order-preserving serial commit of tswap_step
+//                   (tswap.rs:174-286), resumable when a next hop is missing.
+//   K4 k_assign     state machine + nearest-pickup task assignment
+//                   (tswap.rs:106-139), block-parallel argmin, serial order.
+//   k_prequery / k_enqueue_unknown / k_record / occupancy helpers.
+//
+// Launch wrappers are plain C++ functions declared in tsw_launch.h.
+#include <hip/hip_runtime.h>
+
+#include "tsw_internal.h"
+#include "tsw_launch.h"
+
+namespace tsw {
+
+// neighbour directions S,E,N,W = (0,+1),(+1,0),(0,-1),(-1,0): tswap.rs:62
+__device__ __forceinline__ uint32_t step_cell(uint32_t c, uint32_t code, uint32_t W) {
+  switch (code) {
+    case 0: return c + W;
+    case 1: return c + 1;
+    case 2: return c - W;
+    case 3: return c - 1;
+    default: return c;
+  }
+}
+
+// Unreachable-goal fallback of get_path (tswap.rs:378-389): the first
+// neighbour (S,E,N,W order) strictly closer in Manhattan distance; every
+// improving neighbour is exactly 1 closer, so "first improving" == argmin.
+__device__ __forceinline__ uint8_t fallback_code(uint8_t m, uint32_t x, uint32_t y, uint32_t gx,
+                                                 uint32_t gy) {
+  if ((m & 1) && gy > y) return 0;
+  if ((m & 2) && gx > x) return 1;
+  if ((m & 4) && gy < y) return 2;
+  if ((m & 8) && gx < x) return 3;
+  return NH_STAY;
+}
+
+// Next-hop classification from a distance table (any address space).
+__device__ __forceinline__ uint8_t classify_cell(const uint16_t* D, uint32_t c, uint8_t m,
+                                                 uint32_t W, uint32_t goal, uint32_t gx,
+                                                 uint32_t gy) {
+  if (!(m & NB_FREE)) return NH_UNKNOWN;
+  if (c == goal) return NH_STAY;
+  const uint16_t d = D[c];
+  if (d == DIST_INF) return fallback_code(m, c % W, c / W, gx, gy);
+  const uint16_t want = (uint16_t)(d - 1);
+  uint32_t cntc = 0, best = 0;
+#pragma unroll
+  for (uint32_t dir = 0; dir < 4; ++dir) {
+    if (m & (1u << dir)) {
+      if (D[step_cell(c, dir, W)] == want) {
+        ++cntc;
+        best = dir;
+      }
+    }
+  }
+  return cntc == 1 ? (uint8_t)best : NH_UNKNOWN;
+}
+
+__device__ __forceinline__ uint32_t fast_div(uint32_t a, uint32_t b, float inv) {
+  uint32_t q = (uint32_t)((float)a * inv);
+  while (q * b > a) --q;
+  while ((q + 1) * b <= a) ++q;
+  return q;
+}
+
+// ----------------------------------------------------------------------------
+// K1: batched BFS distance tables.
+// One workgroup per goal (grid-stride). LDS holds the frontier bitmap (double
+// buffered), the visited bitmap, the free-cell bitmap and — when LDS_TABLE —
+// the whole u16 table. Each level expands the frontier with word-parallel
+// shifts (east/west inside a row word with carries, north/south from the
+// adjacent rows) over the Manhattan band |y - gy| <= level + 1 only. Newly
+// reached cells get level+1 written into the table. The table then leaves
+// LDS in one pass of 16-B stores together with the 8-B next-hop codes.
+// ----------------------------------------------------------------------------
+template <bool LDS_TABLE>
+__global__ void __launch_bounds__(1024) k_bfs(DevGrid G, const uint32_t* __restrict__ goals,
+                                              const uint32_t* __restrict__ slots, uint32_t k,
+                                              uint16_t* __restrict__ dist_base, uint64_t dstride,
+                                              uint8_t* __restrict__ nh_base, uint64_t nstride,
+                                              uint32_t* __restrict__ err) {
+  extern __shared__ __align__(16) uint32_t smem[];
+  const uint32_t W = G.W, H = G.H, Ww = G.Ww, nw = H * Ww, nwp = (nw + 3u) & ~3u;
+  const uint32_t ncell = G.ncell, ncp = (ncell + 7u) & ~7u;
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  uint32_t* bufA = smem;
+  uint32_t* bufB = smem + nwp;
+  uint32_t* V = smem + 2 * nwp;
+  uint32_t* FR = smem + 3 * nwp;
+  uint16_t* Dl = reinterpret_cast<uint16_t*>(smem + 4 * nwp);
+  const float invWw = 1.0f / (float)Ww;
+  const bool vec_ok = (dstride % 8u) == 0;
+
+  for (uint32_t t = tid; t < nw; t += bd) FR[t] = G.freebits[t];
+
+  for (uint32_t gi = blockIdx.x; gi < k; gi += gridDim.x) {
+    const uint32_t goal = goals[gi];
+    const uint64_t slot = slots ? slots[gi] : gi;
+    uint16_t* Dg = dist_base + slot * dstride;
+    uint16_t* D = LDS_TABLE ? Dl : Dg;
+    for (uint32_t t = tid; t < nw; t += bd) {
+      bufA[t] = 0u;
+      bufB[t] = 0u;
+      V[t] = 0u;
+    }
+    if (LDS_TABLE || vec_ok) {
+      const uint4 inf4 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      const uint32_t lim = LDS_TABLE ? ncp / 8u : ncell / 8u;
+      for (uint32_t t = tid; t < lim; t += bd) reinterpret_cast<uint4*>(D)[t] = inf4;
+      if (!LDS_TABLE)
+        for (uint32_t c = (ncell & ~7u) + tid; c < ncell; c += bd) D[c] = DIST_INF;
+    } else {
+      for (uint32_t c = tid; c < ncell; c += bd) D[c] = DIST_INF;
+    }
+    __syncthreads();
+    const uint32_t gx = goal % W, gy = goal / W;
+    if (tid == 0) {
+      const uint32_t wt = gy * Ww + (gx >> 5);
+      bufA[wt] = 1u << (gx & 31u);
+      V[wt] = 1u << (gx & 31u);
+      D[goal] = 0;
+    }
+    __syncthreads();
+    uint32_t* cur = bufA;
+    uint32_t* nxt = bufB;
+    uint32_t level = 0;
+    for (;;) {
+      const int lo = max(0, (int)gy - (int)level - 1);
+      const int hi = min((int)H - 1, (int)gy + (int)level + 1);
+      const uint32_t t0 = (uint32_t)lo * Ww, t1 = (uint32_t)(hi + 1) * Ww;
+      const uint16_t dn = (uint16_t)(level + 1);
+      int any = 0;
+      for (uint32_t t = t0 + tid; t < t1; t += bd) {
+        const uint32_t r = fast_div(t, Ww, invWw);
+        const uint32_t w = t - r * Ww;
+        const uint32_t f = cur[t];
+        const uint32_t left = (w > 0) ? cur[t - 1] : 0u;
+        const uint32_t right = (w + 1 < Ww) ? cur[t + 1] : 0u;
+        const uint32_t up = (r > 0) ? cur[t - Ww] : 0u;
+        const uint32_t down = (r + 1 < H) ? cur[t + Ww] : 0u;
+        const uint32_t hz = (f << 1) | (left >> 31) | (f >> 1) | (right << 31);
+        uint32_t nb = (hz | up | down) & FR[t] & ~V[t];
+        nxt[t] = nb;
+        if (nb) {
+          V[t] |= nb;
+          any = 1;
+          const uint32_t base = r * W + (w << 5);
+          while (nb) {
+            const uint32_t b = __builtin_ctz(nb);
+            D[base + b] = dn;
+            nb &= nb - 1u;
+          }
+        }
+      }
+      any = __syncthreads_or(any);
+      if (!any) break;
+      ++level;
+      if (level >= 0xFFFEu) {
+        if (tid == 0) atomicOr(err, ERR_DIST_OVERFLOW);
+        break;
+      }
+      uint32_t* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+    }
+    __syncthreads();
+    // write-out (+ fused next-hop classification)
+    uint8_t* NHg = nh_base ? nh_base + slot * nstride : nullptr;
+    if (LDS_TABLE && vec_ok) {
+      for (uint32_t c8 = tid; c8 < ncell / 8u; c8 += bd)
+        reinterpret_cast<uint4*>(Dg)[c8] = reinterpret_cast<const uint4*>(Dl)[c8];
+      for (uint32_t c = (ncell & ~7u) + tid; c < ncell; c += bd) Dg[c] = Dl[c];
+    } else if (LDS_TABLE) {
+      for (uint32_t c = tid; c < ncell; c += bd) Dg[c] = Dl[c];
+    }
+    if (NHg) {
+      for (uint32_t c8 = tid; c8 < ncp / 8u; c8 += bd) {
+        const uint64_t m8 = reinterpret_cast<const uint64_t*>(G.nbmask)[c8];
+        uint64_t codes = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+          const uint32_t c = c8 * 8u + j;
+          uint8_t code = NH_UNKNOWN;
+          if (c < ncell) code = classify_cell(D, c, (uint8_t)(m8 >> (8 * j)), W, goal, gx, gy);
+          codes |= (uint64_t)code << (8 * j);
+        }
+        reinterpret_cast<uint64_t*>(NHg)[c8] = codes;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Next-hop classification for tables that arrived from elsewhere
+// (tsw_import_tables_device): one thread per 8 cells.
+__global__ void k_classify(DevGrid G, const uint32_t* __restrict__ goals,
+                           const uint32_t* __restrict__ slots, uint32_t k,
+                           const uint16_t* __restrict__ dist_base, uint64_t stride,
+                           uint8_t* __restrict__ nh_base) {
+  const uint32_t ncp8 = (G.ncell + 7u) / 8u;
+  const uint64_t total = (uint64_t)k * ncp8;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t gi = (uint32_t)(idx / ncp8), c8 = (uint32_t)(idx % ncp8);
+    const uint32_t goal = goals[gi];
+    const uint64_t slot = slots[gi];
+    const uint16_t* D = dist_base + slot * stride;
+    const uint32_t gx = goal % G.W, gy = goal / G.W;
+    const uint64_t m8 = reinterpret_cast<const uint64_t*>(G.nbmask)[c8];
+    uint64_t codes = 0;
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t c = c8 * 8u + j;
+      uint8_t code = NH_UNKNOWN;
+      if (c < G.ncell) code = classify_cell(D, c, (uint8_t)(m8 >> (8 * j)), G.W, goal, gx, gy);
+      codes |= (uint64_t)code << (8 * j);
+    }
+    reinterpret_cast<uint64_t*>(nh_base + slot * stride)[c8] = codes;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// K3: exact A* next hop, one query per lane.
+// Heap entry: f:21 | g:21 | x:11 | y:11; Rust "a <= b" == key(a) >= key(b).
+// g_score word per cell: tag:10 | label:2 | g:20 where label = direction of
+// path[1] from the start. label(child) = dir if parent is the start, else
+// label(parent) at relaxation time; with a consistent heuristic (Manhattan on
+// a 4-grid) a node's g, came_from and hence label are final when it is first
+// popped, and stale pops relax nothing, so label(goal) at the goal's pop ==
+// the direction of path[1] of the reference's came_from chain (tswap.rs:344-355).
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mk_entry(uint32_t f, uint32_t g, uint32_t x, uint32_t y) {
+  return ((uint64_t)f << 43) | ((uint64_t)g << 22) | ((uint64_t)x << 11) | (uint64_t)y;
+}
+__device__ __forceinline__ uint64_t ekey(uint64_t e) { return e >> KEY_SHIFT; }
+
+// BinaryHeap::sift_up(start = 0, pos) with `elem` in the hole.
+__device__ __forceinline__ void heap_sift_up(uint64_t* Hp, uint32_t pos, uint64_t elem) {
+  const uint64_t k = ekey(elem);
+  while (pos > 0) {
+    const uint32_t parent = (pos - 1u) >> 1;
+    const uint64_t pe = Hp[parent];
+    if (k >= ekey(pe)) break;  // elem <= parent
+    Hp[pos] = pe;
+    pos = parent;
+  }
+  Hp[pos] = elem;
+}
+
+// BinaryHeap::pop with sift_down_to_bottom(0).
+__device__ __forceinline__ uint64_t heap_pop(uint64_t* Hp, uint32_t& len) {
+  const uint32_t end = --len;
+  const uint64_t last = Hp[end];
+  if (end == 0) return last;
+  const uint64_t top = Hp[0];
+  uint32_t pos = 0, child = 1;
+  while (child + 1u < end) {  // child <= end - 2
+    uint64_t l = Hp[child];
+    const uint64_t r = Hp[child + 1];
+    if (ekey(l) >= ekey(r)) {  // left <= right: take the right child
+      ++child;
+      l = r;
+    }
+    Hp[pos] = l;
+    pos = child;
+    child = 2u * pos + 1u;
+  }
+  if (child == end - 1u) {
+    Hp[pos] = Hp[child];
+    pos = child;
+  }
+  heap_sift_up(Hp, pos, last);
+  return top;
+}
+
+__device__ uint8_t astar_one(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag, uint64_t* Hp,
+                             uint32_t hcap, uint32_t* GS, int32_t* len_out, uint32_t* err) {
+  const uint32_t W = G.W;
+  const uint32_t vx = v % W, vy = v / W, gx = goal % W, gy = goal / W;
+  if (v == goal) {
+    *len_out = 1;
+    return NH_STAY;
+  }
+  const uint32_t tagw = tag << 22;
+  uint32_t len = 0;
+  GS[v] = tagw;
+  {
+    const uint32_t h0 = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
+    Hp[0] = mk_entry(h0, 0, vx, vy);
+    len = 1;
+  }
+  while (len > 0) {
+    const uint64_t e = heap_pop(Hp, len);
+    const uint32_t cx = (uint32_t)(e >> 11) & 0x7FFu, cy = (uint32_t)e & 0x7FFu;
+    const uint32_t cg = (uint32_t)(e >> 22) & 0x1FFFFFu;
+    const uint32_t c = cy * W + cx;
+    if (c == goal) {
+      *len_out = (int32_t)cg + 1;
+      return (uint8_t)((GS[goal] >> 20) & 3u);
+    }
+    const uint8_t m = G.nbmask[c];
+    const uint32_t labc = (GS[c] >> 20) & 3u;
+    const uint32_t tg = cg + 1u;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+      if (!(m & (1u << d))) continue;
+      const uint32_t nx = d == 1 ? cx + 1 : (d == 3 ? cx - 1 : cx);
+      const uint32_t ny = d == 0 ? cy + 1 : (d == 2 ? cy - 1 : cy);
+      const uint32_t nc = ny * W + nx;
+      const uint32_t old = GS[nc];
+      const uint32_t oldg = ((old & 0xFFC00000u) == tagw) ? (old & GS_G_MASK) : 0xFFFFFFFFu;
+      if (tg < oldg) {
+        const uint32_t lab = cg == 0 ? d : labc;
+        GS[nc] = tagw | (lab << 20) | tg;
+        if (len >= hcap) {
+          atomicOr(err, ERR_HEAP_OVERFLOW);
+          *len_out = -1;
+          return NH_UNKNOWN;
+        }
+        const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
+        heap_sift_up(Hp, len, mk_entry(tg + h, tg, nx, ny));
+        ++len;
+      }
+    }
+  }
+  *len_out = 2;
+  return fallback_code(G.nbmask[v], vx, vy, gx, gy);
+}
+
+__global__ void __launch_bounds__(64) k_astar(DevGrid G, const AstarQuery* __restrict__ Q,
+                                              const uint32_t* __restrict__ nq_dev, uint32_t nq_host,
+                                              uint8_t* __restrict__ nh_base, uint64_t nstride,
+                                              uint8_t* __restrict__ res, int32_t* __restrict__ lens,
+                                              uint64_t* __restrict__ heaps, uint32_t hcap,
+                                              uint32_t* __restrict__ gs_all, uint32_t* __restrict__ epochs,
+                                              uint32_t nslots, uint32_t* __restrict__ err) {
+  const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= nslots) return;
+  const uint32_t nq = nq_dev ? *nq_dev : nq_host;
+  if (slot >= nq) return;
+  uint64_t* Hp = heaps + (uint64_t)slot * hcap;
+  uint32_t* GS = gs_all + (uint64_t)slot * G.ncell;
+  uint32_t ep = epochs[slot];
+  for (uint32_t qi = slot; qi < nq; qi += nslots) {
+    if (ep % 1023u == 0u && ep > 0u)
+      for (uint32_t c = 0; c < G.ncell; ++c) GS[c] = 0u;
+    const uint32_t tag = ep % 1023u + 1u;
+    ++ep;
+    const AstarQuery q = Q[qi];
+    int32_t L = 0;
+    const uint8_t code = astar_one(G, q.v, q.goal, tag, Hp, hcap, GS, &L, err);
+    if (res) res[q.out] = code;
+    if (lens) lens[q.out] = L;
+    if (nh_base && q.tab >= 0) nh_base[(uint64_t)q.tab * nstride + q.v] = code;
+  }
+  epochs[slot] = ep;
+}
+
+// Enqueue every agent whose current (v, g) next hop is unresolved.
+__global__ void k_prequery(AgentsDev A, const int32_t* __restrict__ goal_tab, uint8_t* __restrict__ nh,
+                           uint64_t nstride, AstarQuery* __restrict__ Q, uint32_t* __restrict__ qcount,
+                           uint32_t* __restrict__ err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const uint32_t v = A.v[i], g = A.g[i];
+  if (v == g) return;
+  const int32_t tab = goal_tab[g];
+  if (tab < 0) {
+    atomicOr(err, ERR_NO_TABLE);
+    return;
+  }
+  uint8_t* p = nh + (uint64_t)tab * nstride + v;
+  if (*p != NH_UNKNOWN) return;
+  *p = NH_PENDING;
+  const uint32_t idx = atomicAdd(qcount, 1u);
+  AstarQuery q;
+  q.v = v;
+  q.goal = g;
+  q.tab = tab;
+  q.out = idx;
+  Q[idx] = q;
+}
+
+// Enqueue every unresolved (goal, cell) of the given table slots (eager mode).
+__global__ void k_enqueue_unknown(DevGrid G, const uint32_t* __restrict__ goals,
+                                  const uint32_t* __restrict__ slots, uint32_t k,
+                                  uint8_t* __restrict__ nh, uint64_t nstride, AstarQuery* __restrict__ Q,
+                                  uint32_t* __restrict__ qcount, uint32_t qcap) {
+  const uint64_t total = (uint64_t)k * G.ncell;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t gi = (uint32_t)(idx / G.ncell), c = (uint32_t)(idx % G.ncell);
+    const uint32_t slot = slots[gi];
+    uint8_t* p = nh + (uint64_t)slot * nstride + c;
+    if (*p != NH_UNKNOWN) continue;
+    if (!(G.nbmask[c] & NB_FREE)) continue;
+    const uint32_t qi = atomicAdd(qcount, 1u);
+    if (qi >= qcap) continue;  // host sees count > cap and retries
+    *p = NH_PENDING;
+    AstarQuery q;
+    q.v = c;
+    q.goal = goals[gi];
+    q.tab = (int32_t)slot;
+    q.out = qi;
+    Q[qi] = q;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// K2: serial commit of tswap_step in agent order, resumable.
+// ----------------------------------------------------------------------------
+struct WalkCtx {
+  AgentsDev A;
+  const int32_t* goal_tab;
+  const uint8_t* nh;
+  uint64_t nstride;
+  uint32_t W;
+};
+
+// get_path(v, g)[1] via the next-hop tables; returns -1 when unresolved.
+__device__ __forceinline__ int resolve_nh(const WalkCtx& C, uint32_t v, uint32_t g, uint32_t* next) {
+  if (v == g) {
+    *next = v;
+    return 1;
+  }
+  const int32_t tab = C.goal_tab[g];
+  if (tab < 0) return -1;
+  const uint8_t code = C.nh[(uint64_t)tab * C.nstride + v];
+  if (code > NH_STAY) return -1;
+  *next = step_cell(v, code, C.W);
+  return 2;
+}
+
+// lowest index agent at `cell` (position(), tswap.rs:192/223/269), rebuilt
+// by a scan only when duplicates share the cell.
+__device__ void occ_rescan(const AgentsDev& A, uint32_t cell) {
+  int32_t best = -1;
+  for (uint32_t k = 0; k < A.n; ++k)
+    if (A.v[k] == cell) {
+      best = (int32_t)k;
+      break;
+    }
+  A.occ[cell] = best;
+}
+
+__device__ void occ_move(const AgentsDev& A, uint32_t i, uint32_t from, uint32_t to) {
+  A.v[i] = to;
+  A.cnt[from] -= 1u;
+  A.cnt[to] += 1u;
+  if (A.cnt[to] == 1u) A.occ[to] = (int32_t)i;
+  else if ((int32_t)i < A.occ[to]) A.occ[to] = (int32_t)i;
+  if (A.occ[from] == (int32_t)i) {
+    if (A.cnt[from] == 0u) A.occ[from] = -1;
+    else occ_rescan(A, from);
+  }
+}
+
+// agents i (at a) and j (at b) exchange cells (tswap.rs:274-277)
+__device__ void occ_swap(const AgentsDev& A, uint32_t i, uint32_t j) {
+  const uint32_t a = A.v[i], b = A.v[j];
+  A.v[i] = b;
+  A.v[j] = a;
+  if (A.cnt[a] == 1u) A.occ[a] = (int32_t)j;
+  else occ_rescan(A, a);
+  if (A.cnt[b] == 1u) A.occ[b] = (int32_t)i;
+  else occ_rescan(A, b);
+}
+
+__global__ void k_walk(WalkCtx C, WalkState* __restrict__ wsp, uint32_t* __restrict__ err) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const AgentsDev& A = C.A;
+  WalkState ws = *wsp;
+  const uint32_t n = A.n;
+  ws.status = 0;
+  if (ws.phase == 0) {
+    // rules phase, tswap.rs:180-252
+    while (ws.i < n) {
+      const uint32_t i = ws.i;
+      if (!ws.in_chase) {
+        const uint32_t vi = A.v[i], gi = A.g[i];
+        if (vi == gi) {  // rule 1
+          ++ws.i;
+          continue;
+        }
+        uint32_t u;
+        if (resolve_nh(C, vi, gi, &u) < 0) {
+          ws.status = 1;
+          ws.miss_agent = i;
+          goto save;
+        }
+        const int32_t j = A.occ[u];
+        if (j < 0 || (uint32_t)j == i) {
+          ++ws.i;
+          continue;
+        }
+        const uint32_t vj = A.v[j], gj = A.g[j];
+        if (vj == gj) {  // rule 3: goal swap
+          A.g[i] = gj;
+          A.g[j] = gi;
+          ++ws.i;
+          continue;
+        }
+        // rule 4: start the deadlock chase, a_p = [i]
+        ws.in_chase = 1;
+        ws.chase_id += 1u;
+        A.stamp[i] = ws.chase_id;
+        A.ap[0] = i;
+        ws.ap_len = 1;
+        ws.b = (uint32_t)j;
+      }
+      {
+        bool found = false;
+        for (;;) {
+          const uint32_t b = ws.b;
+          const uint32_t bv = A.v[b], bg = A.g[b];
+          if (bv == bg) break;
+          uint32_t w;
+          if (resolve_nh(C, bv, bg, &w) < 0) {
+            ws.status = 1;
+            ws.miss_agent = b;
+            goto save;
+          }
+          const int32_t c = A.occ[w];
+          if (c < 0) break;
+          if (A.stamp[b] == ws.chase_id) {  // a_p.contains(b): clear
+            ws.ap_len = 0;
+            break;
+          }
+          A.ap[ws.ap_len++] = b;
+          A.stamp[b] = ws.chase_id;
+          ws.b = (uint32_t)c;
+          if ((uint32_t)c == i) {
+            found = true;
+            break;
+          }
+        }
+        if (found && ws.ap_len > 1) {  // rotate targets, tswap.rs:241-249
+          const uint32_t L = ws.ap_len;
+          const uint32_t last_goal = A.g[A.ap[L - 1]];
+          for (uint32_t kk = L - 1; kk >= 1; --kk) A.g[A.ap[kk]] = A.g[A.ap[kk - 1]];
+          A.g[A.ap[0]] = last_goal;
+        }
+        ws.in_chase = 0;
+        ++ws.i;
+      }
+    }
+    ws.phase = 1;
+    ws.i = 0;
+  }
+  if (ws.phase == 1) {
+    // movement phase, tswap.rs:257-285
+    while (ws.i < n) {
+      const uint32_t i = ws.i;
+      const uint32_t vi = A.v[i], gi = A.g[i];
+      if (vi == gi) {
+        ++ws.i;
+        continue;
+      }
+      uint32_t u;
+      if (resolve_nh(C, vi, gi, &u) < 0) {
+        ws.status = 1;
+        ws.miss_agent = i;
+        goto save;
+      }
+      const int32_t j = A.occ[u];
+      if (j < 0) {
+        occ_move(A, i, vi, u);  // rule 2
+      } else if ((uint32_t)j != i) {
+        const uint32_t vj = A.v[j], gj = A.g[j];
+        if (vj != gj) {
+          uint32_t w;
+          if (resolve_nh(C, vj, gj, &w) < 0) {
+            ws.status = 1;
+            ws.miss_agent = (uint32_t)j;
+            goto save;
+          }
+          if (w == vi) occ_swap(A, i, (uint32_t)j);  // mutual swap
+        }
+      }
+      ++ws.i;
+    }
+    ws.phase = 2;
+  }
+save:
+  *wsp = ws;
+}
+
+// ----------------------------------------------------------------------------
+// K4: state machine + task assignment (tswap.rs:106-139), one workgroup.
+// Agents that can change this step (v == g, or Idle while tasks remain) are
+// compacted in index order; each is then handled in order, the idle ones by
+// a block-wide argmin over unused tasks keyed (manhattan << 32 | task index)
+// so ties resolve to the first minimum as min_by_key does (:130).
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t y = __shfl_xor(x, off, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+__global__ void __launch_bounds__(1024) k_assign(AgentsDev A, TasksDev TK, uint32_t W,
+                                                 uint32_t* __restrict__ done_flag) {
+  __shared__ uint32_t s_list[1024];
+  __shared__ uint32_t s_wcount[16];
+  __shared__ uint64_t s_red[16];
+  __shared__ uint32_t s_unused, s_cnt, s_doit, s_px, s_py;
+  const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6;
+  const uint32_t nwaves = bd >> 6;
+  const uint32_t n = A.n, m = TK.m;
+  if (tid == 0) s_unused = *TK.unused;
+  __syncthreads();
+  for (uint32_t base = 0; base < n; base += bd) {
+    const uint32_t i = base + tid;
+    bool needy = false;
+    if (i < n) needy = (A.v[i] == A.g[i]) || (A.st[i] == ST_IDLE && s_unused > 0u);
+    const uint64_t bal = __ballot(needy);
+    if (lane == 0) s_wcount[wid] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    if (needy) {
+      uint32_t off = 0;
+      for (uint32_t w = 0; w < wid; ++w) off += s_wcount[w];
+      off += (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      s_list[off] = i;
+    }
+    if (tid == 0) {
+      uint32_t c = 0;
+      for (uint32_t w = 0; w < nwaves; ++w) c += s_wcount[w];
+      s_cnt = c;
+    }
+    __syncthreads();
+    const uint32_t cnt = s_cnt;
+    for (uint32_t kk = 0; kk < cnt; ++kk) {
+      const uint32_t ai = s_list[kk];
+      if (tid == 0) {
+        const uint32_t v = A.v[ai];
+        uint8_t st = A.st[ai];
+        if (v == A.g[ai]) {
+          if (st == ST_TO_PICKUP) {
+            st = ST_TO_DELIVERY;
+            const int32_t tk = A.task[ai];
+            if (tk >= 0) A.g[ai] = TK.dlv[tk];
+          } else if (st == ST_TO_DELIVERY) {
+            st = ST_IDLE;
+            A.task[ai] = -1;
+          }
+          A.st[ai] = st;
+        }
+        s_doit = (st == ST_IDLE && s_unused > 0u) ? 1u : 0u;
+        s_px = v % W;
+        s_py = v / W;
+      }
+      __syncthreads();
+      if (s_doit) {
+        const uint32_t px = s_px, py = s_py;
+        uint64_t best = ~0ull;
+        for (uint32_t t = tid; t < m; t += bd) {
+          if (!TK.used[t]) {
+            const uint32_t xy = TK.pick_xy[t];
+            const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
+            const uint32_t d = (px > tx ? px - tx : tx - px) + (py > ty ? py - ty : ty - py);
+            const uint64_t key = ((uint64_t)d << 32) | t;
+            best = key < best ? key : best;
+          }
+        }
+        best = wave_min_u64(best);
+        if (lane == 0) s_red[wid] = best;
+        __syncthreads();
+        if (tid == 0) {
+          uint64_t b = ~0ull;
+          for (uint32_t w = 0; w < nwaves; ++w) b = s_red[w] < b ? s_red[w] : b;
+          if (b != ~0ull) {
+            const uint32_t t = (uint32_t)(b & 0xFFFFFFFFu);
+            TK.used[t] = 1;
+            s_unused -= 1u;
+            A.task[ai] = (int32_t)t;
+            A.st[ai] = ST_TO_PICKUP;
+            A.g[ai] = TK.pick[t];
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // termination test inputs (tswap.rs:163-169): all tasks used && all idle
+  int busy = 0;
+  for (uint32_t i = tid; i < n; i += bd) busy |= (A.st[i] != ST_IDLE);
+  busy = __syncthreads_or(busy);
+  if (tid == 0) {
+    *TK.unused = s_unused;
+    *done_flag = (s_unused == 0u && !busy) ? 1u : 0u;
+  }
+}
+
+// record (tswap.rs:144-158): x | y << 16 | AgentState << 32
+__global__ void k_record(AgentsDev A, uint32_t W, uint64_t* __restrict__ rec, uint32_t* __restrict__ goal_rec) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.n) return;
+  const uint32_t v = A.v[i], g = A.g[i];
+  const uint8_t st = A.st[i];
+  uint64_t s;
+  if (st == ST_IDLE) s = 3;
+  else if (st == ST_TO_PICKUP) s = 0;
+  else s = (v == g) ? 2 : 1;
+  rec[i] = (uint64_t)(v % W) | ((uint64_t)(v / W) << 16) | (s << 32);
+  if (goal_rec) goal_rec[i] = g;
+}
+
+__global__ void k_occ_clear(int32_t* occ, uint32_t* cnt, uint32_t ncell) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < ncell) {
+    occ[c] = 0x7FFFFFFF;
+    cnt[c] = 0u;
+  }
+}
+__global__ void k_occ_build(AgentsDev A) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < A.n) {
+    atomicAdd(&A.cnt[A.v[i]], 1u);
+    atomicMin(&A.occ[A.v[i]], (int32_t)i);
+  }
+}
+__global__ void k_occ_fix(int32_t* occ, uint32_t ncell) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < ncell && occ[c] == 0x7FFFFFFF) occ[c] = -1;
+}
+
+// ---------------------------------------------------------------------------
+// launch wrappers
+// ---------------------------------------------------------------------------
+size_t bfs_lds_bytes(const DevGrid& G, bool lds_table) {
+  const size_t nwp = ((size_t)G.H * G.Ww + 3u) & ~(size_t)3u;
+  size_t b = 4u * nwp * 4u;
+  if (lds_table) b += (((size_t)G.ncell + 7u) & ~(size_t)7u) * 2u;
+  return b;
+}
+
+hipError_t launch_bfs(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
+                      uint16_t* dist_base, uint64_t dstride, uint8_t* nh_base, uint64_t nstride,
+                      uint32_t* err, int max_lds, int num_cu, hipStream_t s) {
+  if (k == 0) return hipSuccess;
+  size_t lds_tab = bfs_lds_bytes(G, true);
+  size_t lds_no = bfs_lds_bytes(G, false);
+  const bool use_tab = lds_tab <= (size_t)max_lds;
+  const size_t lds = use_tab ? lds_tab : lds_no;
+  if (lds > (size_t)max_lds) return hipErrorInvalidValue;
+  const uint32_t nw = G.H * G.Ww;
+  uint32_t bd;
+  if (lds > 80 * 1024) bd = 1024;
+  else if (nw <= 64) bd = 64;
+  else if (nw <= 1024) bd = 256;
+  else bd = 512;
+  const uint32_t per_cu = (uint32_t)std::max<size_t>(1, (160 * 1024) / std::max<size_t>(lds, 1));
+  uint32_t grid = std::min<uint32_t>(k, (uint32_t)num_cu * std::min<uint32_t>(per_cu, 16u) * 4u);
+  if (grid == 0) grid = 1;
+  if (use_tab) {
+    hipFuncSetAttribute((const void*)k_bfs<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_bfs<true>, dim3(grid), dim3(bd), lds, s, G, goals, slots, k, dist_base, dstride,
+                       nh_base, nstride, err);
+  } else {
+    hipFuncSetAttribute((const void*)k_bfs<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_bfs<false>, dim3(grid), dim3(bd), lds, s, G, goals, slots, k, dist_base, dstride,
+                       nh_base, nstride, err);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_classify(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
+                           const uint16_t* dist_base, uint64_t stride, uint8_t* nh_base, hipStream_t s) {
+  if (k == 0) return hipSuccess;
+  const uint64_t total = (uint64_t)k * ((G.ncell + 7u) / 8u);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
+  hipLaunchKernelGGL(k_classify, dim3(grid), dim3(256), 0, s, G, goals, slots, k, dist_base, stride, nh_base);
+  return hipGetLastError();
+}
+
+hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* nq_dev, uint32_t nq_host,
+                        uint32_t launch_threads, uint8_t* nh_base, uint64_t nstride, uint8_t* res,
+                        int32_t* lens, uint64_t* heaps, uint32_t hcap, uint32_t* gs_all, uint32_t* epochs,
+                        uint32_t nslots, uint32_t* err, hipStream_t s) {
+  if (launch_threads == 0) return hipSuccess;
+  const uint32_t th = std::min(launch_threads, nslots);
+  const uint32_t grid = (th + 63) / 64;
+  hipLaunchKernelGGL(k_astar, dim3(grid), dim3(64), 0, s, G, Q, nq_dev, nq_host, nh_base, nstride, res, lens,
+                     heaps, hcap, gs_all, epochs, th, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_prequery(const AgentsDev& A, const int32_t* goal_tab, uint8_t* nh, uint64_t nstride,
+                           AstarQuery* Q, uint32_t* qcount, uint32_t* err, hipStream_t s) {
+  if (A.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prequery, dim3((A.n + 255) / 256), dim3(256), 0, s, A, goal_tab, nh, nstride, Q, qcount,
+                     err);
+  return hipGetLastError();
+}
+
+hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
+                                  uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
+                                  uint32_t qcap, hipStream_t s) {
+  if (k == 0) return hipSuccess;
+  const uint64_t total = (uint64_t)k * G.ncell;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
+  hipLaunchKernelGGL(k_enqueue_unknown, dim3(grid), dim3(256), 0, s, G, goals, slots, k, nh, nstride, Q, qcount,
+                     qcap);
+  return hipGetLastError();
+}
+
+hipError_t launch_walk(const AgentsDev& A, const int32_t* goal_tab, const uint8_t* nh, uint64_t nstride,
+                       uint32_t W, WalkState* ws, uint32_t* err, hipStream_t s) {
+  WalkCtx C;
+  C.A = A;
+  C.goal_tab = goal_tab;
+  C.nh = nh;
+  C.nstride = nstride;
+  C.W = W;
+  hipLaunchKernelGGL(k_walk, dim3(1), dim3(64), 0, s, C, ws, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_assign(const AgentsDev& A, const TasksDev& TK, uint32_t W, uint32_t* done_flag,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_assign, dim3(1), dim3(1024), 0, s, A, TK, W, done_flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_record(const AgentsDev& A, uint32_t W, uint64_t* rec, uint32_t* goal_rec, hipStream_t s) {
+  if (A.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_record, dim3((A.n + 255) / 256), dim3(256), 0, s, A, W, rec, goal_rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_occ_build(const AgentsDev& A, uint32_t ncell, hipStream_t s) {
+  hipLaunchKernelGGL(k_occ_clear, dim3((ncell + 255) / 256), dim3(256), 0, s, A.occ, A.cnt, ncell);
+  if (A.n) hipLaunchKernelGGL(k_occ_build, dim3((A.n + 255) / 256), dim3(256), 0, s, A);
+  hipLaunchKernelGGL(k_occ_fix, dim3((ncell + 255) / 256), dim3(256), 0, s, A.occ, ncell);
+  return hipGetLastError();
+}
+
+}  // namespace tsw

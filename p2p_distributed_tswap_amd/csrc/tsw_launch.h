@@ -1,0 +1,43 @@
+// tsw_launch.h — host-callable launch wrappers for the kernels in tsw_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+
+#include "tsw_internal.h"
+
+namespace tsw {
+
+size_t bfs_lds_bytes(const DevGrid& G, bool lds_table);
+
+hipError_t launch_bfs(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
+                      uint16_t* dist_base, uint64_t dstride, uint8_t* nh_base, uint64_t nstride,
+                      uint32_t* err, int max_lds, int num_cu, hipStream_t s);
+
+hipError_t launch_classify(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
+                           const uint16_t* dist_base, uint64_t stride, uint8_t* nh_base, hipStream_t s);
+
+hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* nq_dev, uint32_t nq_host,
+                        uint32_t launch_threads, uint8_t* nh_base, uint64_t nstride, uint8_t* res,
+                        int32_t* lens, uint64_t* heaps, uint32_t hcap, uint32_t* gs_all, uint32_t* epochs,
+                        uint32_t nslots, uint32_t* err, hipStream_t s);
+
+hipError_t launch_prequery(const AgentsDev& A, const int32_t* goal_tab, uint8_t* nh, uint64_t nstride,
+                           AstarQuery* Q, uint32_t* qcount, uint32_t* err, hipStream_t s);
+
+hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
+                                  uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
+                                  uint32_t qcap, hipStream_t s);
+
+hipError_t launch_walk(const AgentsDev& A, const int32_t* goal_tab, const uint8_t* nh, uint64_t nstride,
+                       uint32_t W, WalkState* ws, uint32_t* err, hipStream_t s);
+
+hipError_t launch_assign(const AgentsDev& A, const TasksDev& TK, uint32_t W, uint32_t* done_flag,
+                         hipStream_t s);
+
+hipError_t launch_record(const AgentsDev& A, uint32_t W, uint64_t* rec, uint32_t* goal_rec, hipStream_t s);
+
+hipError_t launch_occ_build(const AgentsDev& A, uint32_t ncell, hipStream_t s);
+
+}  // namespace tsw

@@ -1,0 +1,193 @@
+"""Seeded synthetic MovingAI-style grids and MAPD instances.
+
+The reference draws starts/tasks with unseeded thread_rng (src/map/make_node.rs:22-49,
+src/map/task_generator.rs:23); every instance here is reproducible from a seed
+through a self-contained splitmix64 stream, so fixtures never depend on a
+library's RNG version. '.' = passable, '@' = blocked (the only blocked char the
+reference recognises, tswap.rs:53). Starts and tasks are drawn from the largest
+4-connected component so that no task is unreachable.
+"""
+from __future__ import annotations
+
+from collections import deque
+
+import numpy as np
+
+MASK64 = (1 << 64) - 1
+
+
+class SplitMix64:
+    def __init__(self, seed: int):
+        self.state = seed & MASK64
+
+    def next_u64(self) -> int:
+        self.state = (self.state + 0x9E3779B97F4A7C15) & MASK64
+        z = self.state
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+        return z ^ (z >> 31)
+
+    def uniform(self) -> float:
+        return (self.next_u64() >> 11) * (1.0 / (1 << 53))
+
+    def below(self, n: int) -> int:
+        return self.next_u64() % n
+
+    def shuffle(self, a: list) -> None:
+        for i in range(len(a) - 1, 0, -1):
+            j = self.below(i + 1)
+            a[i], a[j] = a[j], a[i]
+
+
+def to_rows(arr: np.ndarray) -> list:
+    return ["".join("@" if b else "." for b in row) for row in arr]
+
+
+def rows_to_blocked(rows) -> np.ndarray:
+    return np.array([[c == "@" for c in r] for r in rows], dtype=bool)
+
+
+def bundled_map() -> list:
+    """src/map/map.rs MAP: 100 rows x 100 '.' (parse_map, bin/centralized/manager.rs:25-34)."""
+    return ["." * 100 for _ in range(100)]
+
+
+def open_map(w: int, h: int) -> list:
+    return ["." * w for _ in range(h)]
+
+
+def random_map(w: int, h: int, p: float, seed: int) -> list:
+    """Bernoulli(p) obstacles (random-32-32-20 style)."""
+    r = SplitMix64(seed)
+    blocked = np.zeros((h, w), dtype=bool)
+    for y in range(h):
+        for x in range(w):
+            blocked[y, x] = r.uniform() < p
+    return to_rows(blocked)
+
+
+def warehouse_map(w: int = 170, h: int = 84, seed: int = 0x170084) -> list:
+    """Shelf blocks (2 rows x 10 cols) separated by 1-wide aisles, 2-cell border corridor."""
+    r = SplitMix64(seed)
+    blocked = np.zeros((h, w), dtype=bool)
+    y = 2
+    while y + 2 <= h - 2:
+        x = 2
+        while x + 10 <= w - 2:
+            blocked[y:y + 2, x:x + 10] = True
+            # occasional gap in a shelf row (cross aisle), seeded
+            if r.uniform() < 0.1:
+                gx = x + int(r.below(10))
+                blocked[y:y + 2, gx] = False
+            x += 11
+        y += 3
+    return to_rows(blocked)
+
+
+def cave_map(w: int = 256, h: int = 257, seed: int = 0x520D, fill: float = 0.45, iters: int = 5) -> list:
+    """den520d-like cave: cellular automaton (4-5 rule) on a seeded random fill."""
+    r = SplitMix64(seed)
+    a = np.zeros((h, w), dtype=bool)
+    for y in range(h):
+        for x in range(w):
+            a[y, x] = r.uniform() < fill
+    a[0, :] = a[-1, :] = True
+    a[:, 0] = a[:, -1] = True
+    for _ in range(iters):
+        p = np.pad(a, 1, constant_values=True)
+        cnt = sum(p[1 + dy:1 + dy + h, 1 + dx:1 + dx + w].astype(np.int32)
+                  for dy in (-1, 0, 1) for dx in (-1, 0, 1) if (dy, dx) != (0, 0))
+        a = np.where(a, cnt >= 4, cnt >= 5)
+        a[0, :] = a[-1, :] = True
+        a[:, 0] = a[:, -1] = True
+    return to_rows(a)
+
+
+def sortation_map(w: int = 1024, h: int = 1024) -> list:
+    """Sortation floor: 1-cell chutes (blocked) on a 4-pitch lattice, open aisles between."""
+    a = np.zeros((h, w), dtype=bool)
+    a[2:h - 2:4, 2:w - 2:4] = True
+    return to_rows(a)
+
+
+def largest_component(rows) -> list:
+    """Cells (x, y) of the largest 4-connected free component, row-major order."""
+    blocked = rows_to_blocked(rows)
+    h, w = blocked.shape
+    comp = -np.ones((h, w), dtype=np.int64)
+    best, best_id, cid = 0, -1, 0
+    for sy in range(h):
+        for sx in range(w):
+            if blocked[sy, sx] or comp[sy, sx] >= 0:
+                continue
+            q = deque([(sx, sy)])
+            comp[sy, sx] = cid
+            size = 0
+            while q:
+                x, y = q.popleft()
+                size += 1
+                for dx, dy in ((0, 1), (1, 0), (0, -1), (-1, 0)):
+                    nx, ny = x + dx, y + dy
+                    if 0 <= nx < w and 0 <= ny < h and not blocked[ny, nx] and comp[ny, nx] < 0:
+                        comp[ny, nx] = cid
+                        q.append((nx, ny))
+            if size > best:
+                best, best_id = size, cid
+            cid += 1
+    ys, xs = np.nonzero(comp == best_id)
+    return [(int(x), int(y)) for y, x in zip(ys, xs)]
+
+
+def make_instance(rows, n_agents: int, n_tasks: int, seed: int):
+    """n distinct start cells and n_tasks (pickup != delivery) pairs, seeded.
+
+    Returns (starts (n,2) uint32, tasks (m,4) uint32 [px,py,dx,dy]).
+    """
+    cells = largest_component(rows)
+    r = SplitMix64(seed ^ 0xA5A5A5A5)
+    pool = list(cells)
+    r.shuffle(pool)
+    if n_agents > len(pool):
+        raise ValueError("more agents than free cells")
+    starts = np.array(pool[:n_agents], dtype=np.uint32).reshape(-1, 2)
+    tasks = np.zeros((n_tasks, 4), dtype=np.uint32)
+    nc = len(cells)
+    for k in range(n_tasks):
+        a = r.below(nc)
+        b = r.below(nc - 1)
+        if b >= a:
+            b += 1
+        tasks[k] = (*cells[a], *cells[b])
+    return starts, tasks
+
+
+def rows_to_array(rows) -> np.ndarray:
+    return np.frombuffer("".join(rows).encode("latin-1"), dtype=np.uint8).reshape(len(rows), len(rows[0])).copy()
+
+
+# ---- MovingAI .map I/O --------------------------------
+def write_movingai(path: str, rows) -> None:
+    with open(path, "w") as f:
+        f.write("type octile\n")
+        f.write(f"height {len(rows)}\n")
+        f.write(f"width {len(rows[0])}\n")
+        f.write("map\n")
+        for r in rows:
+            f.write(r + "\n")
+
+
+def read_movingai(path: str, passable: str = ".GS") -> list:
+    """Reads a MovingAI map; any char not in `passable` becomes '@' (blocked)."""
+    with open(path) as f:
+        lines = [ln.rstrip("\r\n") for ln in f]
+    i = lines.index("map")
+    rows = [ln for ln in lines[i + 1:] if ln.strip()]
+    return ["".join(c if c in passable else "@" for c in r).replace("G", ".").replace("S", ".") for r in rows]
+
+
+CONFIGS = {
+    # name: (map factory, n_agents, n_tasks, instance seed)  — BASELINE.json configs
+    "c1_bundled_10": (bundled_map, 10, 30, 1),
+    "c2_random_32_32_20": (lambda: random_map(32, 32, 0.20, 0x3232), 200, 600, 0x3232),
+    "c3_warehouse_170x84": (lambda: warehouse_map(170, 84, 0x170084), 1000, 3000, 0x170084),
+}

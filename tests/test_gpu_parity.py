@@ -1,0 +1,113 @@
+"""GPU parity: HIP path (through the C ABI) vs the CPU oracle, bit-exact."""
+import numpy as np
+import pytest
+
+from p2p_distributed_tswap_amd import Planner, TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP, maps
+from oracle import OracleGraph
+
+pytestmark = pytest.mark.gpu
+
+
+def _grid(name):
+    if name == "open8":
+        return maps.open_map(8, 8)
+    if name == "rand16":
+        return maps.random_map(16, 16, 0.25, 3)
+    if name == "rand32":
+        return maps.random_map(32, 32, 0.20, 0x3232)
+    if name == "bundled":
+        return maps.bundled_map()
+    if name == "warehouse":
+        return maps.warehouse_map(170, 84, 0x170084)
+    if name == "cave":
+        return maps.cave_map(256, 257, 0x520D)
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name,ngoals", [("open8", 64), ("rand32", 300), ("bundled", 64), ("warehouse", 48),
+                                         ("cave", 16)])
+def test_bfs_tables_bit_exact(name, ngoals):
+    rows = _grid(name)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@"))
+    rng = np.random.default_rng(1)
+    goals = rng.choice(free, size=min(ngoals, free.size), replace=False).astype(np.uint32)
+    with Planner(rows) as p:
+        got = p.dist_tables(goals)
+    for k, g in enumerate(goals):
+        ref = og.bfs(int(g))
+        assert np.array_equal(got[k], ref), f"{name} goal {g}: {np.count_nonzero(got[k] != ref)} cells differ"
+
+
+def test_astar_all_pairs_open8():
+    rows = _grid("open8")
+    og = OracleGraph(maps.rows_to_array(rows))
+    s, g = np.meshgrid(np.arange(64), np.arange(64), indexing="ij")
+    s, g = s.reshape(-1).astype(np.uint32), g.reshape(-1).astype(np.uint32)
+    with Planner(rows) as p:
+        nxt, ln = p.get_path_next(s, g)
+    for q in range(s.size):
+        rn, rl, _ = og.get_path_next(int(s[q]), int(g[q]))
+        assert (nxt[q], ln[q]) == (rn, rl), f"query {s[q]}->{g[q]}"
+
+
+@pytest.mark.parametrize("name,nq", [("rand16", 2000), ("rand32", 4000), ("bundled", 1500), ("warehouse", 800)])
+def test_astar_random_pairs(name, nq):
+    rows = _grid(name)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@"))
+    rng = np.random.default_rng(2)
+    s = rng.choice(free, nq).astype(np.uint32)
+    g = rng.choice(free, nq).astype(np.uint32)
+    with Planner(rows) as p:
+        nxt, ln = p.get_path_next(s, g)
+    bad = []
+    for q in range(nq):
+        rn, rl, _ = og.get_path_next(int(s[q]), int(g[q]))
+        if (nxt[q], ln[q]) != (rn, rl):
+            bad.append((int(s[q]), int(g[q]), int(nxt[q]), int(ln[q]), rn, rl))
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("name,n,seed", [("rand16", 40, 1), ("rand32", 200, 2), ("bundled", 60, 3),
+                                          ("warehouse", 300, 4)])
+def test_step_matches_oracle(name, n, seed):
+    rows = _grid(name)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    comp = maps.largest_component(rows)
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(len(comp), size=2 * n, replace=True)
+    cellid = np.array([y * cells.shape[1] + x for (x, y) in comp], dtype=np.uint32)
+    v = cellid[idx[:n]]
+    g = cellid[idx[n:]]
+    g[: n // 5] = v[: n // 5]  # some agents at goal (rule 3 partners)
+    with Planner(rows) as p:
+        for _ in range(6):
+            rv, rg = og.step(v, g)
+            hv, hg = p.step(v, g)
+            assert np.array_equal(hv, rv) and np.array_equal(hg, rg)
+            v, g = rv, rg
+
+
+@pytest.mark.parametrize("name,n,m,seed,flags", [
+    ("rand16", 10, 20, 7, 0),
+    ("rand16", 30, 90, 8, TSW_F_LAZY_NEXTHOP),
+    ("rand32", 200, 600, 0x3232, 0),
+    ("rand32", 120, 300, 5, TSW_F_LAZY_NEXTHOP),
+    ("bundled", 10, 30, 1, 0),
+])
+def test_mapd_matches_oracle(name, n, m, seed, flags):
+    rows = _grid(name)
+    starts, tasks = maps.make_instance(rows, n, m, seed)
+    og = OracleGraph(maps.rows_to_array(rows))
+    ref, rgoal = og.mapd(starts, tasks, 2000, trace_goals=True)
+    with Planner(rows, flags=flags) as p:
+        rec, goal = p.plan_mapd_arrays(starts, tasks, 2000, trace_goals=True)
+    assert rec.shape == ref.shape
+    if not np.array_equal(goal, rgoal):
+        t = int(np.argmax((goal != rgoal).any(axis=0)))
+        pytest.fail(f"goal divergence first at t={t}")
+    assert np.array_equal(rec, ref)
