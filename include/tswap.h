@@ -122,6 +122,10 @@ int tsw_dist_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint
 int tsw_import_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k,
                              const uint16_t *dev_tables);
 
+/* Drop every goal table and next-hop code held by the context (device memory
+ * is kept for reuse). Later calls rebuild what they need. */
+int tsw_clear_tables(tsw_ctx *ctx);
+
 /* Per-context counters and kernel timings (HIP events on the context stream). */
 typedef struct {
     uint64_t bfs_goals, bfs_launches;

@@ -1,7 +1,8 @@
 // tsw_capi.hip — host runtime of the TSWAP planning core behind the C ABI
 // declared in include/tswap.h. Owns device memory, the goal-table store
 // (BFS distances + next-hop codes), the A* scratch slots and the per-step
-// orchestration of K4 (assign) -> [prequery -> K3 (A*) -> K2 (walk)]* -> record.
+// orchestration: K1 tables -> k_plan (persistent K4 assign + K2 step + record),
+// relaunched after each batched K3 (A*) pass over the next hops it could not resolve.
 //
 // Reference call structure being replaced (RenKoya1/p2p_distributed_tswap):
 //   tswap_mapd            src/algorithm/tswap.rs:39-172      -> tsw_plan_mapd
@@ -19,6 +20,7 @@
 
 #include "tsw_internal.h"
 #include "tsw_launch.h"
+#include "tsw_plan.h"
 #include "tswap.h"
 
 using namespace tsw;
@@ -28,7 +30,6 @@ namespace {
 thread_local std::string g_create_err;
 
 struct DevStatus {
-  WalkState ws;
   uint32_t err;
   uint32_t done;
   uint32_t qcount;
@@ -75,14 +76,17 @@ struct tsw_ctx {
 
   DevStatus* d_stat = nullptr;
   DevStatus* h_stat = nullptr;   // pinned, D2H
-  WalkState* h_wsinit = nullptr; // pinned, H2D
+  PlanCtl* d_ctl = nullptr;
+  PlanCtl* h_ctl = nullptr;      // pinned
   uint32_t chase_id = 0;
 
   // agents
   size_t acap = 0;
   uint32_t *d_v = nullptr, *d_g = nullptr, *d_cnt = nullptr, *d_stamp = nullptr, *d_ap = nullptr;
   uint8_t* d_st = nullptr;
-  int32_t *d_task = nullptr, *d_occ = nullptr;
+  int32_t* d_task = nullptr;
+  uint32_t* d_occ = nullptr;
+  uint8_t* d_nhc = nullptr;
   // tasks
   size_t tcap = 0;
   uint32_t *d_pick_xy = nullptr, *d_pick = nullptr, *d_dlv = nullptr, *d_unused = nullptr;
@@ -316,7 +320,7 @@ int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
   std::vector<uint32_t> newg;
   newg.reserve(goals_in.size());
   for (uint32_t g : goals_in)
-    if (c->h_goal_tab[g] < 0) {
+    if (c->h_goal_tab[g] == -1) {
       c->h_goal_tab[g] = -2;  // mark (dedupe)
       newg.push_back(g);
     }
@@ -379,13 +383,14 @@ int ensure_agents(tsw_ctx* c, size_t n) {
   auto fre = [](void* p) {
     if (p) (void)hipFree(p);
   };
-  fre(c->d_v); fre(c->d_g); fre(c->d_stamp); fre(c->d_ap); fre(c->d_st); fre(c->d_task);
+  fre(c->d_v); fre(c->d_g); fre(c->d_stamp); fre(c->d_ap); fre(c->d_st); fre(c->d_task); fre(c->d_nhc);
   HIPCHK(hipMalloc(&c->d_v, cap * 4));
   HIPCHK(hipMalloc(&c->d_g, cap * 4));
   HIPCHK(hipMalloc(&c->d_stamp, cap * 4));
   HIPCHK(hipMemset(c->d_stamp, 0, cap * 4));
   HIPCHK(hipMalloc(&c->d_ap, (cap + 1) * 4));
   HIPCHK(hipMalloc(&c->d_st, cap));
+  HIPCHK(hipMalloc(&c->d_nhc, cap));
   HIPCHK(hipMalloc(&c->d_task, cap * 4));
   if (!c->d_occ) {
     HIPCHK(hipMalloc(&c->d_occ, (size_t)c->G.ncell * 4));
@@ -396,53 +401,79 @@ int ensure_agents(tsw_ctx* c, size_t n) {
   return TSW_OK;
 }
 
-AgentsDev agents_dev(tsw_ctx* c, uint32_t n) {
-  AgentsDev A;
-  A.n = n;
-  A.v = c->d_v;
-  A.g = c->d_g;
-  A.st = c->d_st;
-  A.task = c->d_task;
-  A.occ = c->d_occ;
-  A.cnt = c->d_cnt;
-  A.stamp = c->d_stamp;
-  A.ap = c->d_ap;
-  return A;
+PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_goals) {
+  PlanArgs P{};
+  P.n = n;
+  P.m = m;
+  P.W = c->G.W;
+  P.ncell = c->G.ncell;
+  P.mode = mode;
+  P.v = c->d_v;
+  P.g = c->d_g;
+  P.st = c->d_st;
+  P.task = c->d_task;
+  P.stamp = c->d_stamp;
+  P.nhc = c->d_nhc;
+  P.ap = c->d_ap;
+  P.occ = c->d_occ;
+  P.pick_xy = c->d_pick_xy;
+  P.pick = c->d_pick;
+  P.dlv = c->d_dlv;
+  P.used = c->d_used;
+  P.goal_tab = c->d_goal_tab;
+  P.nh = c->d_nh;
+  P.nstride = c->tstride;
+  P.Q = c->d_Q;
+  P.qcap = (uint32_t)c->qcap;
+  P.rec = c->d_rec;
+  P.grec = want_goals ? c->d_grec : nullptr;
+  P.ctl = c->d_ctl;
+  // LDS residency, in priority order: agents, occupancy grid, task table
+  const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
+  bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
+  bool oc = plan_lds_bytes(n, P.ncell, m, ag, true, false) <= budget;
+  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true) <= budget;
+  P.agents_lds = ag;
+  P.occ_lds = oc;
+  P.tasks_lds = tk;
+  return P;
 }
 
-// One tswap_step: [prequery -> K3 -> K2]* until the walker finishes both phases.
-int run_step_rounds(tsw_ctx* c, const AgentsDev& A) {
-  WalkState ws{};
-  ws.chase_id = c->chase_id;
-  *c->h_wsinit = ws;
-  HIPCHK(hipMemcpyAsync(&c->d_stat->ws, c->h_wsinit, sizeof(WalkState), hipMemcpyHostToDevice, c->s));
-  TRY(ensure_queue(c, std::max<size_t>(A.n, 64)));
-  TRY(ensure_astar_scratch(c));
-  const uint64_t max_rounds = 4ull * A.n + 16;
+// Drive k_plan until it reports done; each NEED_QUERIES exit runs K3 on the queued pairs.
+int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
+  *c->h_ctl = init;
+  HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
+  const size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds);
   for (uint64_t round = 0;; ++round) {
-    if (round > max_rounds) RET(TSW_EINVAL, "walker made no progress");
-    HIPCHK(hipMemsetAsync(&c->d_stat->qcount, 0, 4, c->s));
-    HIPCHK(launch_prequery(A, c->d_goal_tab, c->d_nh, c->tstride, c->d_Q, &c->d_stat->qcount, &c->d_stat->err,
-                           c->s));
-    {
-      Timer t(c, CAT_ASTAR);
-      HIPCHK(launch_astar(c->G, c->d_Q, &c->d_stat->qcount, 0, A.n, c->d_nh, c->tstride, nullptr, nullptr,
-                          c->d_heaps, c->hcap, c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
-    }
-    c->st.astar_launches++;
+    if (round > 16ull * P.n + 4096ull * (init.max_t + 1)) RET(TSW_EINVAL, "plan kernel made no progress");
     {
       Timer t(c, CAT_WALK);
-      HIPCHK(launch_walk(A, c->d_goal_tab, c->d_nh, c->tstride, c->G.W, &c->d_stat->ws, &c->d_stat->err, c->s));
+      HIPCHK(launch_plan(P, lds, c->s));
     }
     c->st.walker_launches++;
-    HIPCHK(hipMemcpyAsync(c->h_stat, c->d_stat, sizeof(DevStatus), hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(PlanCtl), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
-    c->st.astar_queries += c->h_stat->qcount;
-    if (c->h_stat->err) TRY(check_err(c));
-    if (c->h_stat->ws.phase == 2) {
-      c->chase_id = c->h_stat->ws.chase_id;
+    const PlanCtl& k = *c->h_ctl;
+    if (k.err) {
+      char buf[128];
+      snprintf(buf, sizeof buf, "plan kernel error bits 0x%x", k.err);
+      RET((k.err & ERR_NO_TABLE) ? TSW_EINVAL : TSW_EOVERFLOW, buf);
+    }
+    if (k.status == PLAN_DONE) {
+      c->chase_id = k.chase_id;
       return TSW_OK;
     }
+    if (k.status != PLAN_NEED_QUERIES || k.qcount == 0 || k.qcount > P.qcap)
+      RET(TSW_EINVAL, "plan kernel stopped without resolvable next hops");
+    TRY(ensure_astar_scratch(c));
+    {
+      Timer t(c, CAT_ASTAR);
+      HIPCHK(launch_astar(c->G, c->d_Q, nullptr, k.qcount, k.qcount, c->d_nh, c->tstride, nullptr, nullptr,
+                          c->d_heaps, c->hcap, c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
+    }
+    c->st.astar_queries += k.qcount;
+    c->st.astar_launches++;
+    TRY(check_err(c));
   }
 }
 
@@ -505,35 +536,18 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   }
   HIPCHK(hipMemcpyAsync(c->d_unused, &m, 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipStreamSynchronize(c->s));  // host vectors above go out of scope only at return, but keep it simple
-  AgentsDev A = agents_dev(c, n);
-  TasksDev TK;
-  TK.m = m;
-  TK.pick_xy = c->d_pick_xy;
-  TK.pick = c->d_pick;
-  TK.dlv = c->d_dlv;
-  TK.used = c->d_used;
-  TK.unused = c->d_unused;
-  HIPCHK(launch_occ_build(A, c->G.ncell, c->s));
+  HIPCHK(launch_occ(c->d_v, n, c->d_occ, c->d_cnt, c->G.ncell, c->s));
   TRY(ensure_tables(c, goalset));
-
-  uint32_t t = 0;
-  for (;;) {
-    {
-      Timer tm(c, CAT_ASSIGN);
-      HIPCHK(launch_assign(A, TK, c->G.W, &c->d_stat->done, c->s));
-    }
-    c->st.assign_launches++;
-    if (n) TRY(run_step_rounds(c, A));
-    else {
-      HIPCHK(hipMemcpyAsync(c->h_stat, c->d_stat, sizeof(DevStatus), hipMemcpyDeviceToHost, c->s));
-      HIPCHK(hipStreamSynchronize(c->s));
-    }
-    HIPCHK(launch_record(A, c->G.W, c->d_rec + (size_t)t * n, goal_out ? c->d_grec + (size_t)t * n : nullptr,
-                         c->s));
-    ++t;
-    c->st.steps++;
-    if (c->h_stat->done || t > max_t) break;
-  }
+  TRY(ensure_queue(c, std::max<size_t>(n, 64)));
+  PlanArgs P = plan_args(c, n, m, MODE_MAPD, goal_out != nullptr);
+  PlanCtl init{};
+  init.section = SEC_ASSIGN;
+  init.unused = m;
+  init.max_t = max_t;
+  init.chase_id = c->chase_id;
+  TRY(run_plan(c, P, init));
+  const uint32_t t = c->h_ctl->t;
+  c->st.steps += t;
   *out_T = t;
   if (n) {
     std::vector<uint64_t> rec((size_t)t * n);
@@ -642,8 +656,9 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if ((e = hipMemset(c->d_stat, 0, sizeof(DevStatus))) != hipSuccess) return fail("memset status", e);
   if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned status", e);
-  if ((e = hipHostMalloc(&c->h_wsinit, sizeof(WalkState), hipHostMallocDefault)) != hipSuccess)
-    return fail("pinned ws", e);
+  if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
+  if ((e = hipHostMalloc(&c->h_ctl, sizeof(PlanCtl), hipHostMallocDefault)) != hipSuccess)
+    return fail("pinned ctl", e);
   memset(c->h_stat, 0, sizeof(DevStatus));
   size_t freeb = 0, totalb = 0;
   hipMemGetInfo(&freeb, &totalb);
@@ -661,10 +676,10 @@ void tsw_destroy(tsw_ctx* c) {
   fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_stamp); fre(c->d_ap); fre(c->d_st);
-  fre(c->d_task); fre(c->d_occ); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
+  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
   if (c->h_stat) hipHostFree(c->h_stat);
-  if (c->h_wsinit) hipHostFree(c->h_wsinit);
+  if (c->h_ctl) hipHostFree(c->h_ctl);
   for (auto& e : c->pending) {
     hipEventDestroy(e.a);
     hipEventDestroy(e.b);
@@ -702,10 +717,14 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   TRY(ensure_agents(c, n));
   HIPCHK(hipMemcpyAsync(c->d_v, v, n * 4ull, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipMemcpyAsync(c->d_g, g, n * 4ull, hipMemcpyHostToDevice, c->s));
-  AgentsDev A = agents_dev(c, n);
-  HIPCHK(launch_occ_build(A, c->G.ncell, c->s));
+  HIPCHK(launch_occ(c->d_v, n, c->d_occ, c->d_cnt, c->G.ncell, c->s));
   TRY(ensure_tables(c, goals));
-  TRY(run_step_rounds(c, A));
+  TRY(ensure_queue(c, std::max<size_t>(n, 64)));
+  PlanArgs P = plan_args(c, n, 0, MODE_STEP, false);
+  PlanCtl init{};
+  init.section = SEC_PRE1;
+  init.chase_id = c->chase_id;
+  TRY(run_plan(c, P, init));
   HIPCHK(hipMemcpyAsync(v, c->d_v, n * 4ull, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipMemcpyAsync(g, c->d_g, n * 4ull, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipStreamSynchronize(c->s));
@@ -819,7 +838,7 @@ int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, cons
   std::vector<uint32_t> newg, src;
   for (uint32_t i = 0; i < k; ++i) {
     if (!cell_id_ok(c, goals[i])) RET(TSW_EINVAL, "goal cell off-grid or blocked");
-    if (c->h_goal_tab[goals[i]] < 0) {
+    if (c->h_goal_tab[goals[i]] == -1) {
       c->h_goal_tab[goals[i]] = -2;
       newg.push_back(goals[i]);
       src.push_back(i);
@@ -870,6 +889,18 @@ int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, cons
   HIPCHK(hipStreamSynchronize(c->s));
   c->st.tables = c->tab_count;
   if (eager_policy(c, newg.size())) TRY(resolve_all_unknown(c, newg, slots));
+  return TSW_OK;
+}
+
+int tsw_clear_tables(tsw_ctx* c) {
+  if (!c) return TSW_EINVAL;
+  TRY(set_device(c));
+  HIPCHK(hipStreamSynchronize(c->s));
+  std::fill(c->h_goal_tab.begin(), c->h_goal_tab.end(), -1);
+  HIPCHK(hipMemcpyAsync(c->d_goal_tab, c->h_goal_tab.data(), (size_t)c->G.ncell * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  c->tab_count = 0;
+  c->st.tables = 0;
   return TSW_OK;
 }
 

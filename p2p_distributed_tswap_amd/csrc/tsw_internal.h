@@ -12,8 +12,9 @@
 //                                   neighbour), NH_UNKNOWN = needs exact A*
 //   goal_tab[ncell]            i32  goal cell -> table slot (-1 = none)
 //   tab_goal[cap]              u32  table slot -> goal cell
-// Agent state (SoA, n agents): v, g (u32 cell ids), st (u8), task (i32),
-// occ[ncell] (i32 lowest agent index at cell, -1 none), cnt[ncell] (u32).
+// Agent state (SoA, n agents): v, g (u32 cell ids), st (u8), task (i32); occupancy
+// occ[ncell] (u32 lowest agent index at the cell | 0x80000000 if shared, ~0 if empty).
+// Persistent plan kernel arguments / control block: tsw_plan.h.
 #pragma once
 #include <stdint.h>
 
@@ -63,38 +64,5 @@ constexpr uint32_t ERR_DIST_OVERFLOW = 2u;
 constexpr uint32_t ERR_G_OVERFLOW = 4u;
 constexpr uint32_t ERR_NO_TABLE = 8u;
 constexpr uint32_t ERR_WALK_OVERFLOW = 16u;
-
-// serial-commit (walker) resumable state, tswap.rs:180-285
-struct WalkState {
-  uint32_t phase;     // 0 rules, 1 movement, 2 done
-  uint32_t i;         // current agent
-  uint32_t in_chase;  // rule-4 chase in progress
-  uint32_t b;         // current_b_idx
-  uint32_t ap_len;    // len(a_p)
-  uint32_t chase_id;  // membership stamp for a_p.contains()
-  uint32_t status;    // 0 = phase finished, 1 = stopped on an unresolved next hop
-  uint32_t miss_agent;
-};
-
-struct AgentsDev {
-  uint32_t n;
-  uint32_t* v;
-  uint32_t* g;
-  uint8_t* st;
-  int32_t* task;
-  int32_t* occ;
-  uint32_t* cnt;
-  uint32_t* stamp;
-  uint32_t* ap;
-};
-
-struct TasksDev {
-  uint32_t m;
-  const uint32_t* pick_xy;  // x | y << 16
-  const uint32_t* pick;     // cell
-  const uint32_t* dlv;      // cell
-  uint8_t* used;
-  uint32_t* unused;         // single counter
-};
 
 }  // namespace tsw

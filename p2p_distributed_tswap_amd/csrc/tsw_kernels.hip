@@ -7,11 +7,9 @@
 //                   neighbour / unreachable fallback / needs-A*).
 //   K3 k_astar      exact get_path() next hop (tswap.rs:288-390): one query
 //                   per lane, Rust std BinaryHeap sift semantics restated.
-//   K2 k_walk       order-preserving serial commit of tswap_step
-//                   (tswap.rs:174-286), resumable when a next hop is missing.
-//   K4 k_assign     state machine + nearest-pickup task assignment
-//                   (tswap.rs:106-139), block-parallel argmin, serial order.
-//   k_prequery / k_enqueue_unknown / k_record / occupancy helpers.
+//   k_classify      next-hop codes for tables imported from elsewhere.
+//   k_enqueue_unknown  eager next-hop mode: queue every unresolved (cell, goal).
+// K2 (step) and K4 (assignment) live in the persistent k_plan (tsw_plan.hip).
 //
 // Launch wrappers are plain C++ functions declared in tsw_launch.h.
 #include <hip/hip_runtime.h>
@@ -365,31 +363,6 @@ __global__ void __launch_bounds__(64) k_astar(DevGrid G, const AstarQuery* __res
   epochs[slot] = ep;
 }
 
-// Enqueue every agent whose current (v, g) next hop is unresolved.
-__global__ void k_prequery(AgentsDev A, const int32_t* __restrict__ goal_tab, uint8_t* __restrict__ nh,
-                           uint64_t nstride, AstarQuery* __restrict__ Q, uint32_t* __restrict__ qcount,
-                           uint32_t* __restrict__ err) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.n) return;
-  const uint32_t v = A.v[i], g = A.g[i];
-  if (v == g) return;
-  const int32_t tab = goal_tab[g];
-  if (tab < 0) {
-    atomicOr(err, ERR_NO_TABLE);
-    return;
-  }
-  uint8_t* p = nh + (uint64_t)tab * nstride + v;
-  if (*p != NH_UNKNOWN) return;
-  *p = NH_PENDING;
-  const uint32_t idx = atomicAdd(qcount, 1u);
-  AstarQuery q;
-  q.v = v;
-  q.goal = g;
-  q.tab = tab;
-  q.out = idx;
-  Q[idx] = q;
-}
-
 // Enqueue every unresolved (goal, cell) of the given table slots (eager mode).
 __global__ void k_enqueue_unknown(DevGrid G, const uint32_t* __restrict__ goals,
                                   const uint32_t* __restrict__ slots, uint32_t k,
@@ -413,327 +386,6 @@ __global__ void k_enqueue_unknown(DevGrid G, const uint32_t* __restrict__ goals,
     q.out = qi;
     Q[qi] = q;
   }
-}
-
-// ----------------------------------------------------------------------------
-// K2: serial commit of tswap_step in agent order, resumable.
-// ----------------------------------------------------------------------------
-struct WalkCtx {
-  AgentsDev A;
-  const int32_t* goal_tab;
-  const uint8_t* nh;
-  uint64_t nstride;
-  uint32_t W;
-};
-
-// get_path(v, g)[1] via the next-hop tables; returns -1 when unresolved.
-__device__ __forceinline__ int resolve_nh(const WalkCtx& C, uint32_t v, uint32_t g, uint32_t* next) {
-  if (v == g) {
-    *next = v;
-    return 1;
-  }
-  const int32_t tab = C.goal_tab[g];
-  if (tab < 0) return -1;
-  const uint8_t code = C.nh[(uint64_t)tab * C.nstride + v];
-  if (code > NH_STAY) return -1;
-  *next = step_cell(v, code, C.W);
-  return 2;
-}
-
-// lowest index agent at `cell` (position(), tswap.rs:192/223/269), rebuilt
-// by a scan only when duplicates share the cell.
-__device__ void occ_rescan(const AgentsDev& A, uint32_t cell) {
-  int32_t best = -1;
-  for (uint32_t k = 0; k < A.n; ++k)
-    if (A.v[k] == cell) {
-      best = (int32_t)k;
-      break;
-    }
-  A.occ[cell] = best;
-}
-
-__device__ void occ_move(const AgentsDev& A, uint32_t i, uint32_t from, uint32_t to) {
-  A.v[i] = to;
-  A.cnt[from] -= 1u;
-  A.cnt[to] += 1u;
-  if (A.cnt[to] == 1u) A.occ[to] = (int32_t)i;
-  else if ((int32_t)i < A.occ[to]) A.occ[to] = (int32_t)i;
-  if (A.occ[from] == (int32_t)i) {
-    if (A.cnt[from] == 0u) A.occ[from] = -1;
-    else occ_rescan(A, from);
-  }
-}
-
-// agents i (at a) and j (at b) exchange cells (tswap.rs:274-277)
-__device__ void occ_swap(const AgentsDev& A, uint32_t i, uint32_t j) {
-  const uint32_t a = A.v[i], b = A.v[j];
-  A.v[i] = b;
-  A.v[j] = a;
-  if (A.cnt[a] == 1u) A.occ[a] = (int32_t)j;
-  else occ_rescan(A, a);
-  if (A.cnt[b] == 1u) A.occ[b] = (int32_t)i;
-  else occ_rescan(A, b);
-}
-
-__global__ void k_walk(WalkCtx C, WalkState* __restrict__ wsp, uint32_t* __restrict__ err) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const AgentsDev& A = C.A;
-  WalkState ws = *wsp;
-  const uint32_t n = A.n;
-  ws.status = 0;
-  if (ws.phase == 0) {
-    // rules phase, tswap.rs:180-252
-    while (ws.i < n) {
-      const uint32_t i = ws.i;
-      if (!ws.in_chase) {
-        const uint32_t vi = A.v[i], gi = A.g[i];
-        if (vi == gi) {  // rule 1
-          ++ws.i;
-          continue;
-        }
-        uint32_t u;
-        if (resolve_nh(C, vi, gi, &u) < 0) {
-          ws.status = 1;
-          ws.miss_agent = i;
-          goto save;
-        }
-        const int32_t j = A.occ[u];
-        if (j < 0 || (uint32_t)j == i) {
-          ++ws.i;
-          continue;
-        }
-        const uint32_t vj = A.v[j], gj = A.g[j];
-        if (vj == gj) {  // rule 3: goal swap
-          A.g[i] = gj;
-          A.g[j] = gi;
-          ++ws.i;
-          continue;
-        }
-        // rule 4: start the deadlock chase, a_p = [i]
-        ws.in_chase = 1;
-        ws.chase_id += 1u;
-        A.stamp[i] = ws.chase_id;
-        A.ap[0] = i;
-        ws.ap_len = 1;
-        ws.b = (uint32_t)j;
-      }
-      {
-        bool found = false;
-        for (;;) {
-          const uint32_t b = ws.b;
-          const uint32_t bv = A.v[b], bg = A.g[b];
-          if (bv == bg) break;
-          uint32_t w;
-          if (resolve_nh(C, bv, bg, &w) < 0) {
-            ws.status = 1;
-            ws.miss_agent = b;
-            goto save;
-          }
-          const int32_t c = A.occ[w];
-          if (c < 0) break;
-          if (A.stamp[b] == ws.chase_id) {  // a_p.contains(b): clear
-            ws.ap_len = 0;
-            break;
-          }
-          A.ap[ws.ap_len++] = b;
-          A.stamp[b] = ws.chase_id;
-          ws.b = (uint32_t)c;
-          if ((uint32_t)c == i) {
-            found = true;
-            break;
-          }
-        }
-        if (found && ws.ap_len > 1) {  // rotate targets, tswap.rs:241-249
-          const uint32_t L = ws.ap_len;
-          const uint32_t last_goal = A.g[A.ap[L - 1]];
-          for (uint32_t kk = L - 1; kk >= 1; --kk) A.g[A.ap[kk]] = A.g[A.ap[kk - 1]];
-          A.g[A.ap[0]] = last_goal;
-        }
-        ws.in_chase = 0;
-        ++ws.i;
-      }
-    }
-    ws.phase = 1;
-    ws.i = 0;
-  }
-  if (ws.phase == 1) {
-    // movement phase, tswap.rs:257-285
-    while (ws.i < n) {
-      const uint32_t i = ws.i;
-      const uint32_t vi = A.v[i], gi = A.g[i];
-      if (vi == gi) {
-        ++ws.i;
-        continue;
-      }
-      uint32_t u;
-      if (resolve_nh(C, vi, gi, &u) < 0) {
-        ws.status = 1;
-        ws.miss_agent = i;
-        goto save;
-      }
-      const int32_t j = A.occ[u];
-      if (j < 0) {
-        occ_move(A, i, vi, u);  // rule 2
-      } else if ((uint32_t)j != i) {
-        const uint32_t vj = A.v[j], gj = A.g[j];
-        if (vj != gj) {
-          uint32_t w;
-          if (resolve_nh(C, vj, gj, &w) < 0) {
-            ws.status = 1;
-            ws.miss_agent = (uint32_t)j;
-            goto save;
-          }
-          if (w == vi) occ_swap(A, i, (uint32_t)j);  // mutual swap
-        }
-      }
-      ++ws.i;
-    }
-    ws.phase = 2;
-  }
-save:
-  *wsp = ws;
-}
-
-// ----------------------------------------------------------------------------
-// K4: state machine + task assignment (tswap.rs:106-139), one workgroup.
-// Agents that can change this step (v == g, or Idle while tasks remain) are
-// compacted in index order; each is then handled in order, the idle ones by
-// a block-wide argmin over unused tasks keyed (manhattan << 32 | task index)
-// so ties resolve to the first minimum as min_by_key does (:130).
-// ----------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t y = __shfl_xor(x, off, 64);
-    x = y < x ? y : x;
-  }
-  return x;
-}
-
-__global__ void __launch_bounds__(1024) k_assign(AgentsDev A, TasksDev TK, uint32_t W,
-                                                 uint32_t* __restrict__ done_flag) {
-  __shared__ uint32_t s_list[1024];
-  __shared__ uint32_t s_wcount[16];
-  __shared__ uint64_t s_red[16];
-  __shared__ uint32_t s_unused, s_cnt, s_doit, s_px, s_py;
-  const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6;
-  const uint32_t nwaves = bd >> 6;
-  const uint32_t n = A.n, m = TK.m;
-  if (tid == 0) s_unused = *TK.unused;
-  __syncthreads();
-  for (uint32_t base = 0; base < n; base += bd) {
-    const uint32_t i = base + tid;
-    bool needy = false;
-    if (i < n) needy = (A.v[i] == A.g[i]) || (A.st[i] == ST_IDLE && s_unused > 0u);
-    const uint64_t bal = __ballot(needy);
-    if (lane == 0) s_wcount[wid] = (uint32_t)__popcll(bal);
-    __syncthreads();
-    if (needy) {
-      uint32_t off = 0;
-      for (uint32_t w = 0; w < wid; ++w) off += s_wcount[w];
-      off += (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-      s_list[off] = i;
-    }
-    if (tid == 0) {
-      uint32_t c = 0;
-      for (uint32_t w = 0; w < nwaves; ++w) c += s_wcount[w];
-      s_cnt = c;
-    }
-    __syncthreads();
-    const uint32_t cnt = s_cnt;
-    for (uint32_t kk = 0; kk < cnt; ++kk) {
-      const uint32_t ai = s_list[kk];
-      if (tid == 0) {
-        const uint32_t v = A.v[ai];
-        uint8_t st = A.st[ai];
-        if (v == A.g[ai]) {
-          if (st == ST_TO_PICKUP) {
-            st = ST_TO_DELIVERY;
-            const int32_t tk = A.task[ai];
-            if (tk >= 0) A.g[ai] = TK.dlv[tk];
-          } else if (st == ST_TO_DELIVERY) {
-            st = ST_IDLE;
-            A.task[ai] = -1;
-          }
-          A.st[ai] = st;
-        }
-        s_doit = (st == ST_IDLE && s_unused > 0u) ? 1u : 0u;
-        s_px = v % W;
-        s_py = v / W;
-      }
-      __syncthreads();
-      if (s_doit) {
-        const uint32_t px = s_px, py = s_py;
-        uint64_t best = ~0ull;
-        for (uint32_t t = tid; t < m; t += bd) {
-          if (!TK.used[t]) {
-            const uint32_t xy = TK.pick_xy[t];
-            const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
-            const uint32_t d = (px > tx ? px - tx : tx - px) + (py > ty ? py - ty : ty - py);
-            const uint64_t key = ((uint64_t)d << 32) | t;
-            best = key < best ? key : best;
-          }
-        }
-        best = wave_min_u64(best);
-        if (lane == 0) s_red[wid] = best;
-        __syncthreads();
-        if (tid == 0) {
-          uint64_t b = ~0ull;
-          for (uint32_t w = 0; w < nwaves; ++w) b = s_red[w] < b ? s_red[w] : b;
-          if (b != ~0ull) {
-            const uint32_t t = (uint32_t)(b & 0xFFFFFFFFu);
-            TK.used[t] = 1;
-            s_unused -= 1u;
-            A.task[ai] = (int32_t)t;
-            A.st[ai] = ST_TO_PICKUP;
-            A.g[ai] = TK.pick[t];
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // termination test inputs (tswap.rs:163-169): all tasks used && all idle
-  int busy = 0;
-  for (uint32_t i = tid; i < n; i += bd) busy |= (A.st[i] != ST_IDLE);
-  busy = __syncthreads_or(busy);
-  if (tid == 0) {
-    *TK.unused = s_unused;
-    *done_flag = (s_unused == 0u && !busy) ? 1u : 0u;
-  }
-}
-
-// record (tswap.rs:144-158): x | y << 16 | AgentState << 32
-__global__ void k_record(AgentsDev A, uint32_t W, uint64_t* __restrict__ rec, uint32_t* __restrict__ goal_rec) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.n) return;
-  const uint32_t v = A.v[i], g = A.g[i];
-  const uint8_t st = A.st[i];
-  uint64_t s;
-  if (st == ST_IDLE) s = 3;
-  else if (st == ST_TO_PICKUP) s = 0;
-  else s = (v == g) ? 2 : 1;
-  rec[i] = (uint64_t)(v % W) | ((uint64_t)(v / W) << 16) | (s << 32);
-  if (goal_rec) goal_rec[i] = g;
-}
-
-__global__ void k_occ_clear(int32_t* occ, uint32_t* cnt, uint32_t ncell) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < ncell) {
-    occ[c] = 0x7FFFFFFF;
-    cnt[c] = 0u;
-  }
-}
-__global__ void k_occ_build(AgentsDev A) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < A.n) {
-    atomicAdd(&A.cnt[A.v[i]], 1u);
-    atomicMin(&A.occ[A.v[i]], (int32_t)i);
-  }
-}
-__global__ void k_occ_fix(int32_t* occ, uint32_t ncell) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < ncell && occ[c] == 0x7FFFFFFF) occ[c] = -1;
 }
 
 // ---------------------------------------------------------------------------
@@ -797,14 +449,6 @@ hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* n
   return hipGetLastError();
 }
 
-hipError_t launch_prequery(const AgentsDev& A, const int32_t* goal_tab, uint8_t* nh, uint64_t nstride,
-                           AstarQuery* Q, uint32_t* qcount, uint32_t* err, hipStream_t s) {
-  if (A.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_prequery, dim3((A.n + 255) / 256), dim3(256), 0, s, A, goal_tab, nh, nstride, Q, qcount,
-                     err);
-  return hipGetLastError();
-}
-
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
                                   uint32_t qcap, hipStream_t s) {
@@ -813,37 +457,6 @@ hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const
   const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
   hipLaunchKernelGGL(k_enqueue_unknown, dim3(grid), dim3(256), 0, s, G, goals, slots, k, nh, nstride, Q, qcount,
                      qcap);
-  return hipGetLastError();
-}
-
-hipError_t launch_walk(const AgentsDev& A, const int32_t* goal_tab, const uint8_t* nh, uint64_t nstride,
-                       uint32_t W, WalkState* ws, uint32_t* err, hipStream_t s) {
-  WalkCtx C;
-  C.A = A;
-  C.goal_tab = goal_tab;
-  C.nh = nh;
-  C.nstride = nstride;
-  C.W = W;
-  hipLaunchKernelGGL(k_walk, dim3(1), dim3(64), 0, s, C, ws, err);
-  return hipGetLastError();
-}
-
-hipError_t launch_assign(const AgentsDev& A, const TasksDev& TK, uint32_t W, uint32_t* done_flag,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_assign, dim3(1), dim3(1024), 0, s, A, TK, W, done_flag);
-  return hipGetLastError();
-}
-
-hipError_t launch_record(const AgentsDev& A, uint32_t W, uint64_t* rec, uint32_t* goal_rec, hipStream_t s) {
-  if (A.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_record, dim3((A.n + 255) / 256), dim3(256), 0, s, A, W, rec, goal_rec);
-  return hipGetLastError();
-}
-
-hipError_t launch_occ_build(const AgentsDev& A, uint32_t ncell, hipStream_t s) {
-  hipLaunchKernelGGL(k_occ_clear, dim3((ncell + 255) / 256), dim3(256), 0, s, A.occ, A.cnt, ncell);
-  if (A.n) hipLaunchKernelGGL(k_occ_build, dim3((A.n + 255) / 256), dim3(256), 0, s, A);
-  hipLaunchKernelGGL(k_occ_fix, dim3((ncell + 255) / 256), dim3(256), 0, s, A.occ, ncell);
   return hipGetLastError();
 }
 

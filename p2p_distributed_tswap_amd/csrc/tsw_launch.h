@@ -23,21 +23,8 @@ hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* n
                         int32_t* lens, uint64_t* heaps, uint32_t hcap, uint32_t* gs_all, uint32_t* epochs,
                         uint32_t nslots, uint32_t* err, hipStream_t s);
 
-hipError_t launch_prequery(const AgentsDev& A, const int32_t* goal_tab, uint8_t* nh, uint64_t nstride,
-                           AstarQuery* Q, uint32_t* qcount, uint32_t* err, hipStream_t s);
-
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
                                   uint32_t qcap, hipStream_t s);
-
-hipError_t launch_walk(const AgentsDev& A, const int32_t* goal_tab, const uint8_t* nh, uint64_t nstride,
-                       uint32_t W, WalkState* ws, uint32_t* err, hipStream_t s);
-
-hipError_t launch_assign(const AgentsDev& A, const TasksDev& TK, uint32_t W, uint32_t* done_flag,
-                         hipStream_t s);
-
-hipError_t launch_record(const AgentsDev& A, uint32_t W, uint64_t* rec, uint32_t* goal_rec, hipStream_t s);
-
-hipError_t launch_occ_build(const AgentsDev& A, uint32_t ncell, hipStream_t s);
 
 }  // namespace tsw

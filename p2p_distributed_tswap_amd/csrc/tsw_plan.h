@@ -1,0 +1,71 @@
+// tsw_plan.h — arguments and resumable control block of the persistent plan kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "tsw_internal.h"
+
+namespace tsw {
+
+enum : uint32_t {
+  SEC_ASSIGN = 0,
+  SEC_PRE1 = 1,
+  SEC_RULES = 2,
+  SEC_PRE2 = 3,
+  SEC_MOVE = 4,
+  SEC_RECORD = 5,
+  SEC_DONE = 6,
+};
+enum : uint32_t { PLAN_RUNNING = 0, PLAN_NEED_QUERIES = 1, PLAN_DONE = 2, PLAN_ERROR = 3 };
+enum : uint32_t { MODE_MAPD = 0, MODE_STEP = 1 };
+
+// Persisted in device memory between launches (exact resume point).
+struct PlanCtl {
+  uint32_t t;         // timesteps recorded so far
+  uint32_t section;   // SEC_*
+  uint32_t i;         // serial walker: current agent
+  uint32_t in_chase;  // rule-4 chase in progress
+  uint32_t b;         // chase: current_b_idx
+  uint32_t ap_len;    // chase: len(a_p)
+  uint32_t chase_id;  // chase membership stamp
+  uint32_t status;    // PLAN_*
+  uint32_t qcount;    // pairs enqueued for K3
+  uint32_t err;       // ERR_* bits
+  uint32_t unused;    // tasks not yet used
+  uint32_t max_t;     // stop when t > max_t
+  uint32_t miss;      // 1 = unresolved next hop, 2 = goal without table
+  uint32_t steps_run;
+  uint32_t pad0, pad1;
+};
+
+struct PlanArgs {
+  uint32_t n, m, W, ncell;
+  uint32_t mode, agents_lds, occ_lds, tasks_lds;
+  uint32_t* v;
+  uint32_t* g;
+  uint8_t* st;
+  int32_t* task;
+  uint32_t* stamp;
+  uint8_t* nhc;
+  uint32_t* ap;
+  uint32_t* occ;
+  const uint32_t* pick_xy;
+  const uint32_t* pick;
+  const uint32_t* dlv;
+  uint8_t* used;
+  const int32_t* goal_tab;
+  uint8_t* nh;
+  uint64_t nstride;
+  AstarQuery* Q;
+  uint32_t qcap;
+  uint64_t* rec;
+  uint32_t* grec;
+  PlanCtl* ctl;
+};
+
+size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks);
+hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, hipStream_t s);
+hipError_t launch_plan(const PlanArgs& P, size_t lds, hipStream_t s);
+
+}  // namespace tsw

@@ -111,3 +111,42 @@ def test_mapd_matches_oracle(name, n, m, seed, flags):
         t = int(np.argmax((goal != rgoal).any(axis=0)))
         pytest.fail(f"goal divergence first at t={t}")
     assert np.array_equal(rec, ref)
+
+
+@pytest.mark.parametrize("name,n,seed", [("rand16", 30, 11), ("open8", 20, 12)])
+def test_step_duplicate_cells(name, n, seed):
+    """Duplicate agent cells: position() picks the lowest index (tswap.rs:192/269)."""
+    rows = _grid(name)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    comp = maps.largest_component(rows)
+    cellid = np.array([y * cells.shape[1] + x for (x, y) in comp], dtype=np.uint32)
+    rng = np.random.default_rng(seed)
+    v = cellid[rng.choice(len(comp), size=n // 2, replace=True)]
+    v = np.concatenate([v, v[: n - v.size]])  # every cell doubled
+    g = cellid[rng.choice(len(comp), size=n, replace=True)]
+    with Planner(rows) as p:
+        for _ in range(5):
+            rv, rg = og.step(v, g)
+            hv, hg = p.step(v, g)
+            assert np.array_equal(hv, rv) and np.array_equal(hg, rg)
+            v, g = rv, rg
+
+
+@pytest.mark.parametrize("name,n,m,seed,flags", [
+    ("rand32", 200, 600, 0x3232, TSW_F_LAZY_NEXTHOP),
+    ("warehouse", 150, 400, 9, 0),
+    ("bundled", 40, 120, 10, TSW_F_LAZY_NEXTHOP),
+])
+def test_mapd_more(name, n, m, seed, flags):
+    rows = _grid(name)
+    starts, tasks = maps.make_instance(rows, n, m, seed)
+    og = OracleGraph(maps.rows_to_array(rows))
+    ref, rgoal = og.mapd(starts, tasks, 2000, trace_goals=True)
+    with Planner(rows, flags=flags) as p:
+        rec, goal = p.plan_mapd_arrays(starts, tasks, 2000, trace_goals=True)
+    assert rec.shape == ref.shape
+    if not np.array_equal(goal, rgoal):
+        t = int(np.argmax((goal != rgoal).any(axis=0)))
+        pytest.fail(f"goal divergence first at t={t}")
+    assert np.array_equal(rec, ref)
