@@ -139,6 +139,11 @@ typedef struct {
     uint64_t steps;             /* timesteps planned                         */
     uint64_t tables;            /* goal tables resident                      */
     double plan_ms;             /* wall time of the last plan call           */
+    /* inside the persistent plan kernel: device wall time per section, ms:
+     * [0] assign [1] next-hop refresh [2] rules [3] refresh [4] movement
+     * [5] record [6] done/other [7] launch copy-in/out */
+    double plan_section_ms[8];
+    uint64_t rule_rounds;       /* first-firing rounds run by the rules phase */
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

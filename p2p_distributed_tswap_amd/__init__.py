@@ -84,10 +84,13 @@ class Stats(ctypes.Structure):
         ("walker_launches", ctypes.c_uint64), ("walker_ms", ctypes.c_double),
         ("assign_launches", ctypes.c_uint64), ("assign_ms", ctypes.c_double),
         ("steps", ctypes.c_uint64), ("tables", ctypes.c_uint64), ("plan_ms", ctypes.c_double),
+        ("plan_section_ms", ctypes.c_double * 8), ("rule_rounds", ctypes.c_uint64),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["plan_section_ms"] = list(self.plan_section_ms)
+        return d
 
 
 # every symbol declared in include/tswap.h (tests check the .so exports them)

@@ -78,11 +78,22 @@ struct tsw_ctx {
   DevStatus* h_stat = nullptr;   // pinned, D2H
   PlanCtl* d_ctl = nullptr;
   PlanCtl* h_ctl = nullptr;      // pinned
+  unsigned long long* d_ticks = nullptr;
+  int wall_khz = 100000;
   uint32_t chase_id = 0;
 
   // agents
   size_t acap = 0;
-  uint32_t *d_v = nullptr, *d_g = nullptr, *d_cnt = nullptr, *d_stamp = nullptr, *d_ap = nullptr;
+  uint32_t *d_v = nullptr, *d_g = nullptr, *d_cnt = nullptr, *d_succ = nullptr, *d_ap = nullptr;
+  int32_t* d_gt = nullptr;
+  uint8_t* d_dec = nullptr;
+  uint8_t* d_onc = nullptr;
+  uint8_t* d_candc = nullptr;
+  uint32_t* d_f1 = nullptr;
+  uint32_t* d_f2 = nullptr;
+  uint32_t* d_mu = nullptr;
+  uint32_t* d_dups = nullptr;
+  uint32_t* h_dups = nullptr;  // pinned
   uint8_t* d_st = nullptr;
   int32_t* d_task = nullptr;
   uint32_t* d_occ = nullptr;
@@ -383,18 +394,27 @@ int ensure_agents(tsw_ctx* c, size_t n) {
   auto fre = [](void* p) {
     if (p) (void)hipFree(p);
   };
-  fre(c->d_v); fre(c->d_g); fre(c->d_stamp); fre(c->d_ap); fre(c->d_st); fre(c->d_task); fre(c->d_nhc);
+  fre(c->d_v); fre(c->d_g); fre(c->d_succ); fre(c->d_ap); fre(c->d_st); fre(c->d_task); fre(c->d_nhc);
+  fre(c->d_gt); fre(c->d_dec); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
+  HIPCHK(hipMalloc(&c->d_onc, cap));
+  HIPCHK(hipMalloc(&c->d_candc, cap));
+  HIPCHK(hipMalloc(&c->d_f1, (cap + 1) * 4));
+  HIPCHK(hipMalloc(&c->d_f2, (cap + 1) * 4));
   HIPCHK(hipMalloc(&c->d_v, cap * 4));
   HIPCHK(hipMalloc(&c->d_g, cap * 4));
-  HIPCHK(hipMalloc(&c->d_stamp, cap * 4));
-  HIPCHK(hipMemset(c->d_stamp, 0, cap * 4));
+  HIPCHK(hipMalloc(&c->d_succ, cap * 4));
+  HIPCHK(hipMalloc(&c->d_gt, cap * 4));
   HIPCHK(hipMalloc(&c->d_ap, (cap + 1) * 4));
   HIPCHK(hipMalloc(&c->d_st, cap));
   HIPCHK(hipMalloc(&c->d_nhc, cap));
+  HIPCHK(hipMalloc(&c->d_dec, cap));
   HIPCHK(hipMalloc(&c->d_task, cap * 4));
   if (!c->d_occ) {
     HIPCHK(hipMalloc(&c->d_occ, (size_t)c->G.ncell * 4));
     HIPCHK(hipMalloc(&c->d_cnt, (size_t)c->G.ncell * 4));
+    HIPCHK(hipMalloc(&c->d_mu, (size_t)c->G.ncell * 4));
+    HIPCHK(hipMalloc(&c->d_dups, 4));
+    HIPCHK(hipHostMalloc(&c->h_dups, 4, hipHostMallocDefault));
   }
   c->acap = cap;
   c->chase_id = 0;
@@ -412,10 +432,18 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.g = c->d_g;
   P.st = c->d_st;
   P.task = c->d_task;
-  P.stamp = c->d_stamp;
+  P.gt = c->d_gt;
+  P.succ = c->d_succ;
   P.nhc = c->d_nhc;
+  P.dec = c->d_dec;
+  P.onc = c->d_onc;
+  P.candc = c->d_candc;
+  P.f1 = c->d_f1;
+  P.f2 = c->d_f2;
   P.ap = c->d_ap;
   P.occ = c->d_occ;
+  P.mu = c->d_mu;
+  P.has_dups = *c->h_dups;
   P.pick_xy = c->d_pick_xy;
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;
@@ -428,6 +456,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.rec = c->d_rec;
   P.grec = want_goals ? c->d_grec : nullptr;
   P.ctl = c->d_ctl;
+  P.sec_ticks = c->d_ticks;
   // LDS residency, in priority order: agents, occupancy grid, task table
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
@@ -439,16 +468,27 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   return P;
 }
 
+// Occupancy grid in k_plan encoding + whether any cell holds several agents.
+int build_occ(tsw_ctx* c, uint32_t n) {
+  HIPCHK(hipMemsetAsync(c->d_dups, 0, 4, c->s));
+  HIPCHK(launch_occ(c->d_v, n, c->d_occ, c->d_cnt, c->G.ncell, c->d_dups, c->s));
+  HIPCHK(hipMemcpyAsync(c->h_dups, c->d_dups, 4, hipMemcpyDeviceToHost, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  return TSW_OK;
+}
+
 // Drive k_plan until it reports done; each NEED_QUERIES exit runs K3 on the queued pairs.
 int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   *c->h_ctl = init;
   HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
   const size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds);
+  // one lane per agent in the parallel passes when possible; >= 4 waves for the task argmin
+  const uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
   for (uint64_t round = 0;; ++round) {
     if (round > 16ull * P.n + 4096ull * (init.max_t + 1)) RET(TSW_EINVAL, "plan kernel made no progress");
     {
       Timer t(c, CAT_WALK);
-      HIPCHK(launch_plan(P, lds, c->s));
+      HIPCHK(launch_plan(P, lds, block, c->s));
     }
     c->st.walker_launches++;
     HIPCHK(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(PlanCtl), hipMemcpyDeviceToHost, c->s));
@@ -461,6 +501,7 @@ int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     }
     if (k.status == PLAN_DONE) {
       c->chase_id = k.chase_id;
+      c->st.rule_rounds += k.rule_rounds;
       return TSW_OK;
     }
     if (k.status != PLAN_NEED_QUERIES || k.qcount == 0 || k.qcount > P.qcap)
@@ -536,7 +577,7 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   }
   HIPCHK(hipMemcpyAsync(c->d_unused, &m, 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipStreamSynchronize(c->s));  // host vectors above go out of scope only at return, but keep it simple
-  HIPCHK(launch_occ(c->d_v, n, c->d_occ, c->d_cnt, c->G.ncell, c->s));
+  TRY(build_occ(c, n));
   TRY(ensure_tables(c, goalset));
   TRY(ensure_queue(c, std::max<size_t>(n, 64)));
   PlanArgs P = plan_args(c, n, m, MODE_MAPD, goal_out != nullptr);
@@ -657,6 +698,10 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned status", e);
   if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
+  if ((e = hipMalloc(&c->d_ticks, 8 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
+  if ((e = hipMemset(c->d_ticks, 0, 8 * sizeof(unsigned long long))) != hipSuccess) return fail("memset ticks", e);
+  hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, c->device);
+  if (c->wall_khz <= 0) c->wall_khz = 100000;
   if ((e = hipHostMalloc(&c->h_ctl, sizeof(PlanCtl), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned ctl", e);
   memset(c->h_stat, 0, sizeof(DevStatus));
@@ -675,8 +720,10 @@ void tsw_destroy(tsw_ctx* c) {
   };
   fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
-  fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_stamp); fre(c->d_ap); fre(c->d_st);
-  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
+  fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
+  fre(c->d_gt); fre(c->d_dec); fre(c->d_mu); fre(c->d_dups); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
+  if (c->h_dups) (void)hipHostFree(c->h_dups);
+  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
   if (c->h_stat) hipHostFree(c->h_stat);
   if (c->h_ctl) hipHostFree(c->h_ctl);
@@ -717,7 +764,7 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   TRY(ensure_agents(c, n));
   HIPCHK(hipMemcpyAsync(c->d_v, v, n * 4ull, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipMemcpyAsync(c->d_g, g, n * 4ull, hipMemcpyHostToDevice, c->s));
-  HIPCHK(launch_occ(c->d_v, n, c->d_occ, c->d_cnt, c->G.ncell, c->s));
+  TRY(build_occ(c, n));
   TRY(ensure_tables(c, goals));
   TRY(ensure_queue(c, std::max<size_t>(n, 64)));
   PlanArgs P = plan_args(c, n, 0, MODE_STEP, false);
@@ -906,8 +953,13 @@ int tsw_clear_tables(tsw_ctx* c) {
 
 int tsw_get_stats(const tsw_ctx* c, tsw_stats* out) {
   if (!c || !out) return TSW_EINVAL;
-  resolve_timing(const_cast<tsw_ctx*>(c));
+  tsw_ctx* cc = const_cast<tsw_ctx*>(c);
+  resolve_timing(cc);
+  unsigned long long ticks[8] = {0};
+  if (hipSetDevice(c->device) == hipSuccess && hipStreamSynchronize(c->s) == hipSuccess)
+    (void)hipMemcpy(ticks, c->d_ticks, sizeof ticks, hipMemcpyDeviceToHost);
   *out = c->st;
+  for (int k = 0; k < 8; ++k) out->plan_section_ms[k] = (double)ticks[k] / (double)c->wall_khz;
   return TSW_OK;
 }
 
@@ -917,6 +969,7 @@ int tsw_reset_stats(tsw_ctx* c) {
   const uint64_t tabs = c->st.tables;
   c->st = tsw_stats{};
   c->st.tables = tabs;
+  if (c->d_ticks) (void)hipMemset(c->d_ticks, 0, 8 * sizeof(unsigned long long));
   return TSW_OK;
 }
 

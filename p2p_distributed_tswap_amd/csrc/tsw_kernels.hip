@@ -334,6 +334,135 @@ __device__ uint8_t astar_one(const DevGrid& G, uint32_t v, uint32_t goal, uint32
   return fallback_code(G.nbmask[v], vx, vy, gx, gy);
 }
 
+// ----------------------------------------------------------------------------
+// K3 (small grids, ncell <= 1024): the same exact A*, heap in LDS.
+// Heap entry u32: f:11 | g:10 | cell:11 (key = entry >> 11, same order as above);
+// each lane's heap is interleaved with its block-mates (element i of lane t at
+// i*BLK + t), so lanes touching equal heap depths never share an LDS bank.
+// g_score u16 per cell in HBM/L2 per slot: tag:4 | label:2 | g:10.
+// A query whose heap would exceed HCAP is handed to k_astar via the overflow list.
+// ----------------------------------------------------------------------------
+constexpr uint32_t LDS_HCAP = 128;
+constexpr uint32_t LDS_BLK = 256;
+
+__device__ __forceinline__ void lheap_sift_up(uint32_t* Hs, uint32_t t, uint32_t pos, uint32_t elem) {
+  const uint32_t k = elem >> 11;
+  while (pos > 0) {
+    const uint32_t parent = (pos - 1u) >> 1;
+    const uint32_t pe = Hs[parent * LDS_BLK + t];
+    if (k >= (pe >> 11)) break;
+    Hs[pos * LDS_BLK + t] = pe;
+    pos = parent;
+  }
+  Hs[pos * LDS_BLK + t] = elem;
+}
+
+__device__ __forceinline__ uint32_t lheap_pop(uint32_t* Hs, uint32_t t, uint32_t& len) {
+  const uint32_t end = --len;
+  const uint32_t last = Hs[end * LDS_BLK + t];
+  if (end == 0) return last;
+  const uint32_t top = Hs[t];
+  uint32_t pos = 0, child = 1;
+  while (child + 1u < end) {
+    uint32_t l = Hs[child * LDS_BLK + t];
+    const uint32_t r = Hs[(child + 1) * LDS_BLK + t];
+    if ((l >> 11) >= (r >> 11)) {
+      ++child;
+      l = r;
+    }
+    Hs[pos * LDS_BLK + t] = l;
+    pos = child;
+    child = 2u * pos + 1u;
+  }
+  if (child == end - 1u) {
+    Hs[pos * LDS_BLK + t] = Hs[child * LDS_BLK + t];
+    pos = child;
+  }
+  lheap_sift_up(Hs, t, pos, last);
+  return top;
+}
+
+__global__ void __launch_bounds__(LDS_BLK) k_astar_lds(DevGrid G, const AstarQuery* __restrict__ Q, uint32_t nq,
+                                                        uint8_t* __restrict__ nh_base, uint64_t nstride,
+                                                        uint8_t* __restrict__ res, int32_t* __restrict__ lens,
+                                                        uint16_t* __restrict__ gs_all, uint32_t* __restrict__ epochs,
+                                                        uint32_t nslots, AstarQuery* __restrict__ ovf,
+                                                        uint32_t* __restrict__ novf) {
+  __shared__ uint32_t Hs[LDS_HCAP * LDS_BLK];
+  const uint32_t t = threadIdx.x;
+  const uint32_t slot = blockIdx.x * LDS_BLK + t;
+  if (slot >= nslots || slot >= nq) return;
+  const uint32_t W = G.W, ncell = G.ncell;
+  const float invW = 1.0f / (float)W;
+  uint16_t* GS = gs_all + (uint64_t)slot * ncell;
+  uint32_t ep = epochs[slot];
+  for (uint32_t qi = slot; qi < nq; qi += nslots) {
+    if (ep % 15u == 0u && ep > 0u)
+      for (uint32_t c = 0; c < ncell; ++c) GS[c] = 0;
+    const uint32_t tagw = (ep % 15u + 1u) << 12;
+    ++ep;
+    const AstarQuery q = Q[qi];
+    const uint32_t v = q.v, goal = q.goal;
+    const uint32_t vy = fast_div(v, W, invW), vx = v - vy * W;
+    const uint32_t gy = fast_div(goal, W, invW), gx = goal - gy * W;
+    uint8_t code = NH_STAY;
+    int32_t L = 1;
+    if (v != goal) {
+      GS[v] = (uint16_t)tagw;
+      Hs[t] = ((vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy)) << 21 | v;
+      uint32_t len = 1;
+      bool found = false, overflow = false;
+      while (len > 0) {
+        const uint32_t e = lheap_pop(Hs, t, len);
+        const uint32_t c = e & 0x7FFu, cg = (e >> 11) & 0x3FFu;
+        if (c == goal) {
+          code = (uint8_t)((GS[goal] >> 10) & 3u);
+          L = (int32_t)cg + 1;
+          found = true;
+          break;
+        }
+        const uint32_t cy = fast_div(c, W, invW), cx = c - cy * W;
+        const uint8_t m = G.nbmask[c];
+        const uint32_t labc = (GS[c] >> 10) & 3u;
+        const uint32_t tg = cg + 1u;
+#pragma unroll
+        for (uint32_t d = 0; d < 4; ++d) {
+          if (!(m & (1u << d))) continue;
+          const uint32_t nx = d == 1 ? cx + 1 : (d == 3 ? cx - 1 : cx);
+          const uint32_t ny = d == 0 ? cy + 1 : (d == 2 ? cy - 1 : cy);
+          const uint32_t nc = ny * W + nx;
+          const uint32_t old = GS[nc];
+          const uint32_t oldg = ((old & 0xF000u) == tagw) ? (old & 0x3FFu) : 0xFFFFu;
+          if (tg < oldg) {
+            const uint32_t lab = cg == 0 ? d : labc;
+            GS[nc] = (uint16_t)(tagw | (lab << 10) | tg);
+            if (len >= LDS_HCAP) {
+              overflow = true;
+              break;
+            }
+            const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
+            lheap_sift_up(Hs, t, len, ((tg + h) << 21) | (tg << 11) | nc);
+            ++len;
+          }
+        }
+        if (overflow) break;
+      }
+      if (overflow) {
+        ovf[atomicAdd(novf, 1u)] = q;  // resolved by k_astar (global-memory heap)
+        continue;
+      }
+      if (!found) {
+        code = fallback_code(G.nbmask[v], vx, vy, gx, gy);
+        L = 2;
+      }
+    }
+    if (res) res[q.out] = code;
+    if (lens) lens[q.out] = L;
+    if (nh_base && q.tab >= 0) nh_base[(uint64_t)q.tab * nstride + q.v] = code;
+  }
+  epochs[slot] = ep;
+}
+
 __global__ void __launch_bounds__(64) k_astar(DevGrid G, const AstarQuery* __restrict__ Q,
                                               const uint32_t* __restrict__ nq_dev, uint32_t nq_host,
                                               uint8_t* __restrict__ nh_base, uint64_t nstride,
@@ -448,6 +577,19 @@ hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* n
                      heaps, hcap, gs_all, epochs, th, err);
   return hipGetLastError();
 }
+
+hipError_t launch_astar_lds(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
+                            uint8_t* res, int32_t* lens, uint16_t* gs16, uint32_t* epochs, uint32_t nslots,
+                            AstarQuery* ovf, uint32_t* novf, hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  const uint32_t th = std::min(nq, nslots);
+  const uint32_t grid = (th + LDS_BLK - 1) / LDS_BLK;
+  hipLaunchKernelGGL(k_astar_lds, dim3(grid), dim3(LDS_BLK), 0, s, G, Q, nq, nh_base, nstride, res, lens, gs16,
+                     epochs, th, ovf, novf);
+  return hipGetLastError();
+}
+
+bool astar_lds_ok(const DevGrid& G) { return G.ncell <= 1024u; }
 
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,

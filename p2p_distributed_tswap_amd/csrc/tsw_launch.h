@@ -23,6 +23,12 @@ hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* n
                         int32_t* lens, uint64_t* heaps, uint32_t hcap, uint32_t* gs_all, uint32_t* epochs,
                         uint32_t nslots, uint32_t* err, hipStream_t s);
 
+// LDS-heap A* for grids of <= 1024 cells; queries whose heap outgrows LDS land in ovf.
+bool astar_lds_ok(const DevGrid& G);
+hipError_t launch_astar_lds(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
+                            uint8_t* res, int32_t* lens, uint16_t* gs16, uint32_t* epochs, uint32_t nslots,
+                            AstarQuery* ovf, uint32_t* novf, hipStream_t s);
+
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
                                   uint32_t qcap, hipStream_t s);

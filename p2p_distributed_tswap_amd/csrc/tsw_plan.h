@@ -24,32 +24,41 @@ enum : uint32_t { MODE_MAPD = 0, MODE_STEP = 1 };
 struct PlanCtl {
   uint32_t t;         // timesteps recorded so far
   uint32_t section;   // SEC_*
-  uint32_t i;         // serial walker: current agent
-  uint32_t in_chase;  // rule-4 chase in progress
-  uint32_t b;         // chase: current_b_idx
-  uint32_t ap_len;    // chase: len(a_p)
-  uint32_t chase_id;  // chase membership stamp
+  uint32_t i;         // rules: cursor (first agent not yet scanned); movement: DEC initialised
+  uint32_t in_chase;  // (unused, kept for layout)
+  uint32_t b;
+  uint32_t ap_len;
+  uint32_t chase_id;
   uint32_t status;    // PLAN_*
   uint32_t qcount;    // pairs enqueued for K3
   uint32_t err;       // ERR_* bits
   uint32_t unused;    // tasks not yet used
   uint32_t max_t;     // stop when t > max_t
-  uint32_t miss;      // 1 = unresolved next hop, 2 = goal without table
+  uint32_t miss;      // serial movement scan: 1 = unresolved next hop, 2 = goal without table
   uint32_t steps_run;
-  uint32_t pad0, pad1;
+  uint32_t rule_rounds;  // first-firing rounds executed (rules phase)
+  uint32_t pad1;
 };
 
 struct PlanArgs {
   uint32_t n, m, W, ncell;
   uint32_t mode, agents_lds, occ_lds, tasks_lds;
+  uint32_t has_dups, pad0;
   uint32_t* v;
   uint32_t* g;
   uint8_t* st;
   int32_t* task;
-  uint32_t* stamp;
-  uint8_t* nhc;
-  uint32_t* ap;
-  uint32_t* occ;
+  int32_t* gt;    // per agent goal-table slot (global copy, used when agents are not in LDS)
+  uint32_t* succ; // per agent successor / target cell (global copy)
+  uint8_t* nhc;   // per agent next-hop code (global copy)
+  uint8_t* dec;   // per agent movement-round state (persisted across relaunches)
+  uint8_t* onc;   // per agent rule-4 cycle label (global copy)
+  uint8_t* candc; // per agent rule-3 next-hop prefetch (global copy)
+  uint32_t* f1;   // pointer-doubling buffers, n + 1 entries each (global copy)
+  uint32_t* f2;
+  uint32_t* ap;   // rule-4 cycle members
+  uint32_t* occ;  // per cell occupancy
+  uint32_t* mu;   // per cell lowest undecided targeting agent (global copy)
   const uint32_t* pick_xy;
   const uint32_t* pick;
   const uint32_t* dlv;
@@ -62,10 +71,12 @@ struct PlanArgs {
   uint64_t* rec;
   uint32_t* grec;
   PlanCtl* ctl;
+  unsigned long long* sec_ticks;  // [8] wall-clock ticks spent per section (diagnostics)
 };
 
 size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks);
-hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, hipStream_t s);
-hipError_t launch_plan(const PlanArgs& P, size_t lds, hipStream_t s);
+hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, uint32_t* dups,
+                      hipStream_t s);
+hipError_t launch_plan(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s);
 
 }  // namespace tsw

@@ -1,7 +1,7 @@
 // tsw_plan.hip — k_plan: the persistent MAPD planning kernel (K2 step + K4 assignment).
 //
-// One workgroup (16 waves) runs whole timesteps of tswap_mapd (tswap.rs:104-170) on the
-// device without returning to the host:
+// One workgroup runs whole timesteps of tswap_mapd (tswap.rs:104-170) on the device
+// without returning to the host:
 //   ASSIGN  state machine + nearest-pickup assignment (tswap.rs:106-139): needy agents
 //           compacted in index order, block-wide argmin over unused tasks per idle agent
 //   PRE1    parallel next-hop lookup for agents whose (v, g) changed
@@ -15,7 +15,13 @@
 //             target rotation (:199-202, :241-249); cursor moves past it.
 //           Agents that do not fire change nothing, so this equals the sequential scan.
 //   PRE2    parallel lookup for agents whose goal changed
-//   MOVE    serial movement phase (tswap.rs:257-285) on LDS-resident state
+//   MOVE    movement phase (tswap.rs:257-285), exact, as decidability rounds: agent k
+//           commits in a round iff no still-undecided agent a < k can change what k reads
+//           at its turn in the sequential scan — a's target is neither k's target nor
+//           k's cell, a is not the occupant of k's target, and no undecided agent below
+//           k is a pending mutual-swap partner (so no undecided position moves before its
+//           own turn). Decisions read the round-start state, commits are disjoint.
+//           With duplicate start cells the phase runs as the serial scan instead.
 //   RECORD  parallel (Point, AgentState) record (tswap.rs:144-158) + termination (:163-169)
 // When a next hop is unresolved (lazy next-hop mode) the kernel enqueues every such
 // (cell, goal) pair, saves its exact resume point and exits; the host runs K3 (k_astar)
@@ -35,6 +41,9 @@ constexpr uint32_t OCC_FLAG = 0x80000000u;  // cell holds more than one agent (d
 constexpr uint32_t OCC_IDX = 0x7FFFFFFFu;
 constexpr uint32_t SUCC_TERM = 0xFFFFFFFFu;
 constexpr uint32_t NO_AGENT = 0xFFFFFFFFu;
+constexpr uint32_t NO_CELL = 0xFFFFFFFFu;
+// movement-round decision states
+constexpr uint8_t DEC_OPEN = 0, DEC_DONE = 1, DEC_STAY = 2, DEC_MOVE = 3, DEC_SWAP = 4;
 
 __device__ __forceinline__ uint32_t step_cell(uint32_t c, uint32_t code, uint32_t W) {
   switch (code) {
@@ -64,13 +73,21 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
   return x;
 }
 
-// Agent/occupancy arrays; AG / OC select LDS (compile time) so loads are ds_read, not flat.
+// Agent / occupancy arrays; the AG / OC template flags place them in LDS at compile time
+// (ds_read/ds_write instead of flat accesses) when they fit.
 struct Arrays {
-  uint32_t* V;
-  uint32_t* G;
-  uint32_t* SUCC;
-  uint8_t* NHC;
-  uint32_t* OCC;
+  uint32_t* V;     // cell of agent
+  uint32_t* G;     // goal cell of agent
+  int32_t* GT;     // goal-table slot of G (goal_tab[G])
+  uint32_t* SUCC;  // rules: successor agent; movement: target cell
+  uint8_t* NHC;    // next-hop code of (V, G) or NHC_DIRTY
+  uint8_t* DEC;    // movement-round state
+  uint8_t* ONC;    // rules: agent lies on a cycle of succ
+  uint8_t* CANDC;  // rules: next hop of succ(k)'s cell toward k's goal (rule-3 prefetch)
+  uint32_t* F1;    // rules: pointer-doubling buffers (n + 1 entries, n = terminal sink)
+  uint32_t* F2;
+  uint32_t* OCC;   // per cell: lowest agent | OCC_FLAG, or OCC_NONE
+  uint32_t* MU;    // per cell: lowest undecided agent targeting it (movement rounds)
   const uint32_t* PXY;
   uint8_t* USED;
 };
@@ -79,7 +96,7 @@ struct Arrays {
 __device__ __forceinline__ int lookup_code(const PlanArgs& P, const Arrays& S, uint32_t k) {
   const uint8_t c = S.NHC[k];
   if (c <= NH_STAY) return c;
-  const int32_t tab = P.goal_tab[S.G[k]];
+  const int32_t tab = S.GT[k];
   if (tab < 0) return -2;
   const uint8_t code = P.nh[(uint64_t)tab * P.nstride + S.V[k]];
   if (code <= NH_STAY) {
@@ -110,21 +127,60 @@ __device__ __forceinline__ uint32_t succ_of(const PlanArgs& P, const Arrays& S, 
   return o == OCC_NONE ? SUCC_TERM : (o & OCC_IDX);
 }
 
-// Rule 4 test for agent k with succ(k) = s (s != k, s not at goal): does the chase of
-// tswap.rs:205-238 return to k? == k lies on a cycle of succ. Floyd walk from k.
-__device__ __forceinline__ bool on_cycle(const Arrays& S, uint32_t k, uint32_t n) {
-  uint32_t tort = k, hare = k;
-  for (uint32_t it = 0; it <= n; ++it) {
-    hare = S.SUCC[hare];
-    if (hare == SUCC_TERM) return false;
-    if (hare == k) return true;
-    hare = S.SUCC[hare];
-    if (hare == SUCC_TERM) return false;
-    if (hare == k) return true;
-    tort = S.SUCC[tort];
-    if (hare == tort) return false;  // entered a cycle that does not contain k
+// Parallel (whole block): succ of every agent, the rule-4 labels and the rule-3 prefetch.
+// The chase of tswap.rs:205-238 started at j = succ(i) returns to i exactly when i lies on
+// a cycle (length >= 2) of succ over not-at-goal agents. Pointer doubling: after R rounds
+// with 2^R > n, F(k) = succ^(2^R)(k) sits on the cycle k drains into (or the sink n), and
+// succ^(2^R) permutes each cycle, so {F(k)} is exactly the set of cycle members.
+__device__ void rules_init(const PlanArgs& P, const Arrays& S) {
+  const uint32_t tid = threadIdx.x, bd = blockDim.x, n = P.n;
+  for (uint32_t k = tid; k < n; k += bd) {
+    const uint32_t s = succ_of(P, S, k);
+    S.SUCC[k] = s;
+    S.F1[k] = s == SUCC_TERM ? n : s;
+    S.ONC[k] = 0;
+    uint8_t cc = NHC_DIRTY;
+    if (s != SUCC_TERM && s != k && S.V[s] == S.G[s] && S.GT[k] >= 0)
+      cc = P.nh[(uint64_t)S.GT[k] * P.nstride + S.V[s]];
+    S.CANDC[k] = cc;
   }
-  return false;
+  if (tid == 0) {
+    S.F1[n] = n;
+    S.F2[n] = n;
+  }
+  __syncthreads();
+  uint32_t* a = S.F1;
+  uint32_t* b = S.F2;
+  for (uint32_t r = 1; r <= n; r <<= 1) {
+    for (uint32_t k = tid; k < n; k += bd) b[k] = a[a[k]];
+    __syncthreads();
+    uint32_t* t = a;
+    a = b;
+    b = t;
+  }
+  for (uint32_t k = tid; k < n; k += bd) {
+    const uint32_t c = a[k];
+    if (c != n) S.ONC[c] = 1;
+  }
+  __syncthreads();
+}
+
+// Mark the (cell, goal) pair of agent k for K3 if it is not resolved; returns 1 if enqueued.
+__device__ __forceinline__ uint32_t enqueue_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab,
+                                                 uint32_t* s_q) {
+  uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
+  if (*p != NH_UNKNOWN) return 0;  // PENDING: whoever flipped it enqueued it in this pass
+  *p = NH_PENDING;
+  const uint32_t qi = atomicAdd(s_q, 1u);
+  if (qi < P.qcap) {
+    AstarQuery q;
+    q.v = v;
+    q.goal = g;
+    q.tab = tab;
+    q.out = qi;
+    P.Q[qi] = q;
+  }
+  return 1;
 }
 
 // parallel: refresh next-hop codes of agents whose code is dirty; unresolved pairs are
@@ -137,37 +193,21 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
     if (S.NHC[k] <= NH_STAY) continue;
     const uint32_t v = S.V[k], g = S.G[k];
     if (v == g) continue;
-    const int32_t tab = P.goal_tab[g];
+    const int32_t tab = S.GT[k];
     if (tab < 0) {
       atomicOr(&P.ctl->err, ERR_NO_TABLE);
       continue;
     }
-    uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
-    const uint8_t code = *p;
-    if (code <= NH_STAY) {
-      S.NHC[k] = code;
-      continue;
-    }
-    if (code == NH_UNKNOWN) {
-      *p = NH_PENDING;
-      const uint32_t qi = atomicAdd(s_q, 1u);
-      if (qi < P.qcap) {
-        AstarQuery q;
-        q.v = v;
-        q.goal = g;
-        q.tab = tab;
-        q.out = qi;
-        P.Q[qi] = q;
-      }
-    }
-    // NH_PENDING: the agent that flipped it to PENDING in this pass enqueued it.
+    const uint8_t code = P.nh[(uint64_t)tab * P.nstride + v];
+    if (code <= NH_STAY) S.NHC[k] = code;
+    else enqueue_pair(P, v, g, tab, s_q);
   }
   __syncthreads();
   return *s_q;
 }
 
-// Serial movement phase (tswap.rs:257-285); false on an unresolved next hop.
-template <bool AG, bool OC>
+// Serial movement phase (tswap.rs:257-285) — used when cells are shared by several agents
+// (duplicate start cells); false on an unresolved next hop.
 __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
   const uint32_t n = P.n, W = P.W;
   uint32_t i = ctl.i;
@@ -221,11 +261,13 @@ template <bool AG, bool OC>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q, s_cnt, s_doit, s_px, s_py, s_exit, s_best;
+  __shared__ uint32_t s_q, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
+  __shared__ unsigned long long s_tick[8], s_tlast;
+  __shared__ uint32_t s_tsec;
   const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6, nwaves = bd >> 6;
-  const uint32_t n = P.n;
+  const uint32_t n = P.n, W = P.W;
 
   // ---- carve LDS (order must match plan_lds_bytes) ---------------------------
   Arrays S;
@@ -239,16 +281,33 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   if constexpr (AG) {
     S.V = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
     S.G = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
+    S.GT = reinterpret_cast<int32_t*>(carve((size_t)n * 4));
     S.SUCC = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
+    S.F1 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
+    S.F2 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
     S.NHC = carve(n);
+    S.DEC = carve(n);
+    S.ONC = carve(n);
+    S.CANDC = carve(n);
   } else {
     S.V = P.v;
     S.G = P.g;
-    S.SUCC = P.stamp;
+    S.GT = P.gt;
+    S.SUCC = P.succ;
+    S.F1 = P.f1;
+    S.F2 = P.f2;
     S.NHC = P.nhc;
+    S.DEC = P.dec;
+    S.ONC = P.onc;
+    S.CANDC = P.candc;
   }
-  if constexpr (OC) S.OCC = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
-  else S.OCC = P.occ;
+  if constexpr (OC) {
+    S.OCC = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
+    S.MU = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
+  } else {
+    S.OCC = P.occ;
+    S.MU = P.mu;
+  }
   if (P.tasks_lds) {
     uint32_t* pxy = reinterpret_cast<uint32_t*>(carve((size_t)P.m * 4));
     S.USED = carve(P.m);
@@ -262,10 +321,13 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     S.USED = P.used;
   }
   for (uint32_t k = tid; k < n; k += bd) {
+    const uint32_t g = P.g[k];
     if constexpr (AG) {
       S.V[k] = P.v[k];
-      S.G[k] = P.g[k];
+      S.G[k] = g;
+      S.DEC[k] = P.dec[k];
     }
+    S.GT[k] = P.goal_tab[g];
     S.NHC[k] = NHC_DIRTY;
   }
   if constexpr (OC)
@@ -274,6 +336,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_ctl = *P.ctl;
     s_ctl.status = PLAN_RUNNING;
     s_exit = 0;
+    for (int k = 0; k < 8; ++k) s_tick[k] = 0;
+    s_tlast = wall_clock64();
+    s_tsec = 7;  // entry / copy-in
   }
   __syncthreads();
   if (s_ctl.section == SEC_RULES || s_ctl.section == SEC_MOVE) {
@@ -290,6 +355,12 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   for (;;) {
     if (s_exit) break;
     const uint32_t sec = s_ctl.section;
+    if (tid == 0) {
+      const unsigned long long now = wall_clock64();
+      s_tick[s_tsec] += now - s_tlast;
+      s_tlast = now;
+      s_tsec = sec < 7 ? sec : 6;
+    }
     if (sec == SEC_ASSIGN) {
       // ---- K4: state machine + task assignment (tswap.rs:106-139) -------------
       for (uint32_t base = 0; base < n; base += bd) {
@@ -325,7 +396,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                 st = ST_TO_DELIVERY;
                 const int32_t tk = P.task[ai];
                 if (tk >= 0) {
-                  S.G[ai] = P.dlv[tk];
+                  const uint32_t ng = P.dlv[tk];
+                  S.G[ai] = ng;
+                  S.GT[ai] = P.goal_tab[ng];
                   S.NHC[ai] = NHC_DIRTY;
                 }
               } else if (st == ST_TO_DELIVERY) {
@@ -335,8 +408,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
               P.st[ai] = st;
             }
             s_doit = (st == ST_IDLE && s_ctl.unused > 0u) ? 1u : 0u;
-            s_px = v % P.W;
-            s_py = v / P.W;
+            s_px = v % W;
+            s_py = v / W;
           }
           __syncthreads();
           if (s_doit) {
@@ -364,7 +437,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                 s_ctl.unused -= 1u;
                 P.task[ai] = (int32_t)t;
                 P.st[ai] = ST_TO_PICKUP;
-                S.G[ai] = P.pick[t];
+                const uint32_t ng = P.pick[t];
+                S.G[ai] = ng;
+                S.GT[ai] = P.goal_tab[ng];
                 S.NHC[ai] = NHC_DIRTY;
               }
             }
@@ -388,19 +463,27 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         __syncthreads();
         break;
       }
-      if (tid == 0) s_ctl.section = sec == SEC_PRE1 ? SEC_RULES : SEC_MOVE;
+      if (tid == 0) {
+        s_ctl.section = sec == SEC_PRE1 ? SEC_RULES : SEC_MOVE;
+        s_ctl.i = 0;
+      }
       __syncthreads();
     } else if (sec == SEC_RULES) {
       // ---- rules phase as "first firing agent" rounds (see header) ------------
-      for (uint32_t k = tid; k < n; k += bd) S.SUCC[k] = succ_of(P, S, k);
-      __syncthreads();
+      // Cycle labels ONC (k lies on a cycle of succ) come from pointer doubling once per
+      // phase and after rotations; a rule-3 swap (b, s) is folded in incrementally: b's
+      // new goal is the adjacent cell it already targets (same next hop, same succ), and
+      // s — terminal until now — gains one out-edge, so the only new cycle possible is
+      // one through s. CANDC[k] prefetches s's next hop toward k's goal for every rule-3
+      // candidate k, so a swap needs no global round trip on the serial path.
+      rules_init(P, S);
       for (;;) {
         const uint32_t cursor = s_ctl.i;
         uint32_t best = NO_AGENT;
         for (uint32_t k = cursor + tid; k < n; k += bd) {
           const uint32_t s = S.SUCC[k];
           if (s == SUCC_TERM || s == k) continue;
-          if (S.V[s] == S.G[s] || on_cycle(S, k, n)) {
+          if (S.V[s] == S.G[s] || S.ONC[k]) {
             best = k;  // later k of this thread are larger
             break;
           }
@@ -412,46 +495,79 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           uint32_t b = NO_AGENT;
           for (uint32_t w = 0; w < nwaves; ++w) b = s_wcount[w] < b ? s_wcount[w] : b;
           s_best = b;
+          s_miss = 0;
           if (b != NO_AGENT) {
             const uint32_t s = S.SUCC[b];
             if (S.V[s] == S.G[s]) {  // rule 3: goal swap (tswap.rs:198-202)
+              uint32_t code = S.CANDC[b];
+              if (code > NH_STAY && S.GT[b] >= 0) code = P.nh[(uint64_t)S.GT[b] * P.nstride + S.V[s]];
               const uint32_t gb = S.G[b];
+              const int32_t tb = S.GT[b];
               S.G[b] = S.G[s];
+              S.GT[b] = S.GT[s];
               S.G[s] = gb;
-              S.NHC[b] = NHC_DIRTY;
-              S.NHC[s] = NHC_DIRTY;
+              S.GT[s] = tb;
+              S.CANDC[s] = NHC_DIRTY;
+              if (S.V[b] == S.G[b]) S.SUCC[b] = SUCC_TERM;  // shared start cell: b now at its goal
+              if (code <= NH_STAY) {
+                S.NHC[s] = (uint8_t)code;
+                const uint32_t ns = succ_of(P, S, s);
+                S.SUCC[s] = ns;
+                if (ns != SUCC_TERM && ns != s) {
+                  // new cycle through s?
+                  uint32_t x = ns;
+                  for (uint32_t it = 0; it < n && x != SUCC_TERM && x != s; ++it) x = S.SUCC[x];
+                  if (x == s) {
+                    uint32_t y = s;
+                    do {
+                      S.ONC[y] = 1;
+                      y = S.SUCC[y];
+                    } while (y != s);
+                  }
+                }
+              } else {
+                S.NHC[s] = NHC_DIRTY;  // unresolved: refresh + full relabel below
+                s_miss = 1;
+              }
             } else {  // rule 4: rotate targets along the cycle b -> s -> ... -> last -> b
               uint32_t L = 0;
               for (uint32_t a = b; L == 0 || a != b; a = S.SUCC[a]) P.ap[L++] = a;
-              const uint32_t last_goal = S.G[P.ap[L - 1]];
+              const uint32_t last = P.ap[L - 1];
+              const uint32_t last_goal = S.G[last];
+              const int32_t last_tab = S.GT[last];
               for (uint32_t kk = L - 1; kk >= 1; --kk) {
-                const uint32_t a = P.ap[kk];
-                S.G[a] = S.G[P.ap[kk - 1]];
+                const uint32_t a = P.ap[kk], pa = P.ap[kk - 1];
+                S.G[a] = S.G[pa];
+                S.GT[a] = S.GT[pa];
                 S.NHC[a] = NHC_DIRTY;
               }
               S.G[b] = last_goal;
+              S.GT[b] = last_tab;
               S.NHC[b] = NHC_DIRTY;
+              s_miss = 1;  // members' next hops changed: refresh + full relabel below
             }
             s_ctl.i = b + 1;
+            s_ctl.rule_rounds += 1;
           } else {
             s_ctl.i = n;
           }
         }
         __syncthreads();
         if (s_best == NO_AGENT) break;
-        // goals of the fired agents changed: their next hops (hence succ) must be looked up
-        const uint32_t q = refresh_codes(P, S, &s_q);
-        if (q > 0) {
-          if (tid == 0) {
-            s_ctl.qcount = q;
-            s_ctl.status = PLAN_NEED_QUERIES;
-            s_exit = 1;
+        if (s_miss) {
+          // goals of the fired agents changed: their next hops (hence succ) must be looked up
+          const uint32_t q = refresh_codes(P, S, &s_q);
+          if (q > 0) {
+            if (tid == 0) {
+              s_ctl.qcount = q;
+              s_ctl.status = PLAN_NEED_QUERIES;
+              s_exit = 1;
+            }
+            __syncthreads();
+            break;
           }
-          __syncthreads();
-          break;
+          rules_init(P, S);
         }
-        for (uint32_t k = tid; k < n; k += bd) S.SUCC[k] = succ_of(P, S, k);
-        __syncthreads();
       }
       if (s_exit) break;
       if (tid == 0) {
@@ -459,10 +575,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         s_ctl.i = 0;
       }
       __syncthreads();
-    } else if (sec == SEC_MOVE) {
+    } else if (sec == SEC_MOVE && P.has_dups) {
       if (tid == 0) {
         s_ctl.miss = 0;
-        if (walk_move<AG, OC>(P, S, s_ctl)) {
+        if (walk_move(P, S, s_ctl)) {
           s_ctl.section = SEC_RECORD;
           s_ctl.i = 0;
         }
@@ -470,7 +586,6 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       }
       __syncthreads();
       if (s_ctl.miss) {
-        // enqueue every dirty agent's unresolved pair, then return to the host
         const uint32_t q = refresh_codes(P, S, &s_q);
         if (tid == 0) {
           s_ctl.qcount = q;
@@ -480,6 +595,139 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         __syncthreads();
         break;
       }
+    } else if (sec == SEC_MOVE) {
+      // ---- movement phase as decidability rounds (see header) -----------------
+      if (s_ctl.i == 0) {
+        for (uint32_t k = tid; k < n; k += bd) S.DEC[k] = (S.V[k] == S.G[k]) ? DEC_DONE : DEC_OPEN;
+        __syncthreads();
+        if (tid == 0) s_ctl.i = 1;  // DEC initialised for this step (survives relaunches)
+      }
+      for (;;) {
+        if (tid == 0) {
+          s_q = 0;
+          s_miss = 0;
+        }
+        __syncthreads();
+        // A: target cell of every open agent; reset MU at its target and its own cell
+        int open = 0;
+        for (uint32_t k = tid; k < n; k += bd) {
+          if (S.DEC[k] != DEC_OPEN) continue;
+          open = 1;
+          const int code = lookup_code(P, S, k);
+          if (code < 0) {
+            if (code == -2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
+            else enqueue_pair(P, S.V[k], S.G[k], S.GT[k], &s_q);
+            s_miss = 1;
+            S.SUCC[k] = NO_CELL;
+            continue;
+          }
+          const uint32_t v = S.V[k], u = step_cell(v, (uint32_t)code, W);
+          S.SUCC[k] = u;
+          S.MU[u] = NO_AGENT;
+          S.MU[v] = NO_AGENT;
+        }
+        open = __syncthreads_or(open);
+        if (!open) break;
+        if (s_miss) break;  // exit to K3 below
+        // B: lowest open agent targeting each cell
+        for (uint32_t k = tid; k < n; k += bd)
+          if (S.DEC[k] == DEC_OPEN) atomicMin(&S.MU[S.SUCC[k]], k);
+        __syncthreads();
+        // C: lowest open agent whose cell is wanted by an open mutual partner below it
+        uint32_t sp = NO_AGENT;
+        for (uint32_t k = tid; k < n; k += bd) {
+          if (S.DEC[k] != DEC_OPEN) continue;
+          const uint32_t o = S.OCC[S.SUCC[k]];
+          if (o == OCC_NONE) continue;
+          const uint32_t b = o & OCC_IDX;
+          if (b < k && S.DEC[b] == DEC_OPEN && S.SUCC[b] == S.V[k]) {
+            sp = k;
+            break;
+          }
+        }
+        sp = wave_min_u32(sp);
+        if (lane == 0) s_wcount[wid] = sp;
+        __syncthreads();
+        if (tid == 0) {
+          uint32_t b = NO_AGENT;
+          for (uint32_t w = 0; w < nwaves; ++w) b = s_wcount[w] < b ? s_wcount[w] : b;
+          s_best = b;
+        }
+        __syncthreads();
+        const uint32_t spmin = s_best;
+        // D: decide (reads the round-start state only)
+        for (uint32_t k = tid; k < n && k < spmin; k += bd) {
+          if (S.DEC[k] != DEC_OPEN) continue;
+          const uint32_t u = S.SUCC[k], v = S.V[k];
+          if (S.MU[u] != k) continue;
+          if (S.MU[v] < k) continue;
+          const uint32_t o = S.OCC[u];
+          uint8_t act;
+          if (o == OCC_NONE) {
+            act = DEC_MOVE;  // rule 2
+          } else {
+            const uint32_t j = o & OCC_IDX;
+            if (j == k) {
+              act = DEC_STAY;
+            } else {
+              const uint8_t dj = S.DEC[j];
+              if (j < k && dj != DEC_DONE) continue;  // occupant still open below k
+              if (S.V[j] == S.G[j]) {
+                act = DEC_STAY;
+              } else {
+                const int cj = lookup_code(P, S, j);
+                if (cj < 0) {
+                  if (cj == -2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
+                  else enqueue_pair(P, S.V[j], S.G[j], S.GT[j], &s_q);
+                  s_miss = 1;
+                  continue;
+                }
+                act = step_cell(S.V[j], (uint32_t)cj, W) == v ? DEC_SWAP : DEC_STAY;  // :273
+              }
+            }
+          }
+          S.DEC[k] = act;
+        }
+        __syncthreads();
+        // E: commit (disjoint cells by construction)
+        for (uint32_t k = tid; k < n; k += bd) {
+          const uint8_t d = S.DEC[k];
+          if (d < DEC_STAY) continue;
+          S.DEC[k] = DEC_DONE;
+          if (d == DEC_STAY) continue;
+          const uint32_t u = S.SUCC[k], v = S.V[k];
+          if (d == DEC_MOVE) {
+            S.V[k] = u;
+            S.OCC[u] = k;
+            S.OCC[v] = OCC_NONE;
+            S.NHC[k] = NHC_DIRTY;
+          } else {
+            const uint32_t j = S.OCC[u] & OCC_IDX;
+            S.V[k] = u;
+            S.V[j] = v;
+            S.OCC[u] = k;
+            S.OCC[v] = j;
+            S.NHC[k] = NHC_DIRTY;
+            S.NHC[j] = NHC_DIRTY;
+          }
+        }
+        __syncthreads();
+        if (s_miss) break;
+      }
+      if (s_miss) {
+        if (tid == 0) {
+          s_ctl.qcount = s_q;
+          s_ctl.status = s_q > 0 ? PLAN_NEED_QUERIES : PLAN_ERROR;
+          s_exit = 1;
+        }
+        __syncthreads();
+        break;
+      }
+      if (tid == 0) {
+        s_ctl.section = SEC_RECORD;
+        s_ctl.i = 0;
+      }
+      __syncthreads();
     } else if (sec == SEC_RECORD) {
       if (P.mode == MODE_STEP) {
         if (tid == 0) {
@@ -503,7 +751,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         else if (st == ST_TO_PICKUP) s = 0;
         else s = (v == g) ? 2 : 1;
         busy |= (st != ST_IDLE);
-        rec[i] = (uint64_t)(v % P.W) | ((uint64_t)(v / P.W) << 16) | (s << 32);
+        rec[i] = (uint64_t)(v % W) | ((uint64_t)(v / W) << 16) | (s << 32);
         if (grec) grec[i] = g;
       }
       busy = __syncthreads_or(busy);
@@ -530,6 +778,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     for (uint32_t k = tid; k < n; k += bd) {
       P.v[k] = S.V[k];
       P.g[k] = S.G[k];
+      P.dec[k] = S.DEC[k];
     }
   if constexpr (OC)
     for (uint32_t c = tid; c < P.ncell; c += bd) P.occ[c] = S.OCC[c];
@@ -537,6 +786,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     const uint32_t err = P.ctl->err;
     *P.ctl = s_ctl;
     P.ctl->err |= err;
+    s_tick[s_tsec] += wall_clock64() - s_tlast;
+    if (P.sec_ticks)
+      for (int k = 0; k < 8; ++k) P.sec_ticks[k] += s_tick[k];
   }
 }
 
@@ -555,41 +807,45 @@ __global__ void k_occ_add(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t
     atomicMin(&occ[v[i]], i);
   }
 }
-__global__ void k_occ_flag(uint32_t* occ, const uint32_t* cnt, uint32_t ncell) {
+__global__ void k_occ_flag(uint32_t* occ, const uint32_t* cnt, uint32_t ncell, uint32_t* dups) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < ncell && cnt[c] > 1u) occ[c] |= OCC_FLAG;
+  if (c < ncell && cnt[c] > 1u) {
+    occ[c] |= OCC_FLAG;
+    *dups = 1u;
+  }
 }
 
 size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks) {
   auto r16 = [](size_t b) { return (b + 15u) & ~(size_t)15u; };
   size_t b = r16(1024 * 4);
-  if (agents) b += 3 * r16((size_t)n * 4) + r16(n);
-  if (occ) b += r16((size_t)ncell * 4);
+  if (agents) b += 4 * r16((size_t)n * 4) + 2 * r16((size_t)(n + 1) * 4) + 4 * r16(n);
+  if (occ) b += 2 * r16((size_t)ncell * 4);
   if (tasks) b += r16((size_t)m * 4) + r16(m);
   return b;
 }
 
-hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, hipStream_t s) {
+hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, uint32_t* dups,
+                      hipStream_t s) {
   hipLaunchKernelGGL(k_occ_init, dim3((ncell + 255) / 256), dim3(256), 0, s, occ, cnt, ncell);
   if (n) hipLaunchKernelGGL(k_occ_add, dim3((n + 255) / 256), dim3(256), 0, s, v, n, occ, cnt);
-  hipLaunchKernelGGL(k_occ_flag, dim3((ncell + 255) / 256), dim3(256), 0, s, occ, cnt, ncell);
+  hipLaunchKernelGGL(k_occ_flag, dim3((ncell + 255) / 256), dim3(256), 0, s, occ, cnt, ncell, dups);
   return hipGetLastError();
 }
 
 template <bool AG, bool OC>
-static hipError_t launch_plan_t(const PlanArgs& P, size_t lds, hipStream_t s) {
+static hipError_t launch_plan_t(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s) {
   hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_plan<AG, OC>), dim3(1), dim3(1024), lds, s, P);
+  hipLaunchKernelGGL((k_plan<AG, OC>), dim3(1), dim3(block), lds, s, P);
   return hipGetLastError();
 }
 
-hipError_t launch_plan(const PlanArgs& P, size_t lds, hipStream_t s) {
-  if (P.agents_lds && P.occ_lds) return launch_plan_t<true, true>(P, lds, s);
-  if (P.agents_lds) return launch_plan_t<true, false>(P, lds, s);
-  if (P.occ_lds) return launch_plan_t<false, true>(P, lds, s);
-  return launch_plan_t<false, false>(P, lds, s);
+hipError_t launch_plan(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s) {
+  if (P.agents_lds && P.occ_lds) return launch_plan_t<true, true>(P, lds, block, s);
+  if (P.agents_lds) return launch_plan_t<true, false>(P, lds, block, s);
+  if (P.occ_lds) return launch_plan_t<false, true>(P, lds, block, s);
+  return launch_plan_t<false, false>(P, lds, block, s);
 }
 
 }  // namespace tsw
