@@ -122,6 +122,12 @@ int tsw_dist_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint
 int tsw_import_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k,
                              const uint16_t *dev_tables);
 
+/* Next-hop codes of k goal tables (building them if needed), one byte per cell,
+ * row-major: 0..3 = path[1] is the S,E,N,W neighbour (tswap.rs:62 order), 4 = stay
+ * (unreachable goal, no closer neighbour), 0xFF = not resolved yet (lazy mode:
+ * needs the exact A*). out: host buffer k*w*h. */
+int tsw_next_hop_tables(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint8_t *out);
+
 /* Drop every goal table and next-hop code held by the context (device memory
  * is kept for reuse). Later calls rebuild what they need. */
 int tsw_clear_tables(tsw_ctx *ctx);

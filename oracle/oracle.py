@@ -40,6 +40,8 @@ def lib():
         L.orc_get_path_next.restype = i32
         L.orc_bfs_u16.argtypes = [ctypes.c_void_p, u32, P(ctypes.c_uint16)]
         L.orc_bfs_u16.restype = ctypes.c_int
+        L.orc_next_codes.argtypes = [ctypes.c_void_p, u32, P(ctypes.c_uint8)]
+        L.orc_next_codes.restype = ctypes.c_int
         L.orc_tswap_step.argtypes = [ctypes.c_void_p, P(u32), P(u32), u32]
         L.orc_tswap_mapd.argtypes = [ctypes.c_void_p, P(u32), u32, P(u32), u32, u32, P(u64), P(u32)]
         L.orc_tswap_mapd.restype = i32
@@ -79,6 +81,12 @@ class OracleGraph:
         out = np.zeros(self.w * self.h, dtype=np.uint16)
         rc = lib().orc_bfs_u16(self.ptr, goal, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)))
         if rc != 0:
+            raise ValueError("goal blocked")
+        return out
+
+    def next_codes(self, goal: int) -> np.ndarray:
+        out = np.zeros(self.w * self.h, dtype=np.uint8)
+        if lib().orc_next_codes(self.ptr, goal, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))) != 0:
             raise ValueError("goal blocked")
         return out
 

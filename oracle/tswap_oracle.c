@@ -228,6 +228,27 @@ int32_t orc_get_path_next(orc_graph *gr, uint32_t start, uint32_t goal,
     return 2;
 }
 
+/* Next-hop code of get_path(c, goal) for every free cell c (0..3 = S,E,N,W neighbour,
+ * 4 = path[1] == c, i.e. c == goal or the fallback found no closer neighbour);
+ * blocked cells get 0xFF. Checker for the device next-hop tables. */
+int orc_next_codes(orc_graph *gr, uint32_t goal, uint8_t *out) {
+    if (goal >= gr->ncell || !gr->free_[goal]) return -1;
+    for (uint32_t c = 0; c < gr->ncell; c++) {
+        if (!gr->free_[c]) {
+            out[c] = 0xFF;
+            continue;
+        }
+        uint32_t nx;
+        orc_get_path_next(gr, c, goal, &nx, NULL);
+        if (nx == c) out[c] = 4;
+        else if (nx == c + gr->w) out[c] = 0;
+        else if (nx == c + 1) out[c] = 1;
+        else if (nx + gr->w == c) out[c] = 2;
+        else out[c] = 3;
+    }
+    return 0;
+}
+
 int orc_bfs_u16(orc_graph *gr, uint32_t goal, uint16_t *out) {
     if (goal >= gr->ncell || !gr->free_[goal]) return -1;
     for (uint32_t c = 0; c < gr->ncell; c++) out[c] = 0xFFFF;

@@ -45,6 +45,10 @@ int32_t orc_get_path_next(orc_graph *gr, uint32_t start, uint32_t goal,
  * oracle for the K1 kernel: d_g(v) == len(get_path(v,g)) - 1.) */
 int orc_bfs_u16(orc_graph *gr, uint32_t goal, uint16_t *out);
 
+/* get_path(c, goal)[1] for every cell as a direction code (0..3 S,E,N,W, 4 = stay,
+ * 0xFF blocked) — checker for the device next-hop tables. */
+int orc_next_codes(orc_graph *gr, uint32_t goal, uint8_t *out);
+
 /* One tswap_step (tswap.rs:174-286) over agents with cell ids v[i], g[i]
  * (in/out). Order = array order, exactly as the reference. */
 int orc_tswap_step(orc_graph *gr, uint32_t *v, uint32_t *g, uint32_t n);

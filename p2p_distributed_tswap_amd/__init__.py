@@ -97,7 +97,7 @@ class Stats(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "tsw_create", "tsw_destroy", "tsw_last_error", "tsw_plan_mapd", "tsw_plan_mapd_trace",
     "tsw_step", "tsw_get_path_next", "tsw_dist_tables", "tsw_dist_tables_device",
-    "tsw_import_tables_device", "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing",
+    "tsw_import_tables_device", "tsw_next_hop_tables", "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing",
 )
 
 _lib = None
@@ -128,11 +128,12 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_dist_tables_device.argtypes = [vp, P(u32), u32, vp]
     lib.tsw_import_tables_device.argtypes = [vp, P(u32), u32, vp]
     lib.tsw_clear_tables.argtypes = [vp]
+    lib.tsw_next_hop_tables.argtypes = [vp, P(u32), u32, P(ctypes.c_uint8)]
     lib.tsw_get_stats.argtypes = [vp, P(Stats)]
     lib.tsw_reset_stats.argtypes = [vp]
     lib.tsw_set_timing.argtypes = [vp, ctypes.c_int]
     for name in ("tsw_plan_mapd", "tsw_plan_mapd_trace", "tsw_step", "tsw_get_path_next", "tsw_dist_tables",
-                 "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats",
+                 "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_clear_tables", "tsw_next_hop_tables", "tsw_get_stats", "tsw_reset_stats",
                  "tsw_set_timing"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
@@ -270,6 +271,13 @@ class Planner:
     def import_tables_device(self, goals, dev_ptr: int):
         g = np.ascontiguousarray(goals, dtype=np.uint32)
         self._check(self._lib.tsw_import_tables_device(self._ctx, _u32p(g), g.size, ctypes.c_void_p(dev_ptr)))
+
+    def next_hop_tables(self, goals) -> np.ndarray:
+        g = np.ascontiguousarray(goals, dtype=np.uint32)
+        out = np.zeros((g.size, self.h * self.w), dtype=np.uint8)
+        self._check(self._lib.tsw_next_hop_tables(self._ctx, _u32p(g), g.size,
+                                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out
 
     def clear_tables(self):
         self._check(self._lib.tsw_clear_tables(self._ctx))

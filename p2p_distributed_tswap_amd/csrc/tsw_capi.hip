@@ -33,7 +33,7 @@ struct DevStatus {
   uint32_t err;
   uint32_t done;
   uint32_t qcount;
-  uint32_t pad;
+  uint32_t novf;  // LDS A*: queries handed to the global-heap kernel
 };
 
 enum { CAT_BFS = 0, CAT_ASTAR = 1, CAT_WALK = 2, CAT_ASSIGN = 3, NCAT = 4 };
@@ -66,6 +66,11 @@ struct tsw_ctx {
   uint64_t* d_heaps = nullptr;
   uint32_t* d_gs = nullptr;
   uint32_t* d_epochs = nullptr;
+  uint32_t nslots16 = 0;  // LDS-heap A* (small grids)
+  uint16_t* d_gs16 = nullptr;
+  uint32_t* d_ep16 = nullptr;
+  AstarQuery* d_ovf = nullptr;
+  size_t ovf_cap = 0;
 
   // query queue
   AstarQuery* d_Q = nullptr;
@@ -146,7 +151,7 @@ struct tsw_ctx {
 namespace {
 
 template <class T>
-hipError_t dgrow(T*& p, size_t& cap, size_t need, bool zero = false) {
+hipError_t dgrow(T*& p, size_t& cap, size_t need) {
   if (need <= cap && p) return hipSuccess;
   if (p) {
     hipError_t e = hipFree(p);
@@ -161,7 +166,6 @@ hipError_t dgrow(T*& p, size_t& cap, size_t need, bool zero = false) {
     return e;
   }
   cap = nc;
-  if (zero) return hipMemset(p, 0, nc * sizeof(T));
   return hipSuccess;
 }
 
@@ -251,9 +255,11 @@ int ensure_astar_scratch(tsw_ctx* c) {
   c->nslots = (uint32_t)ns;
   HIPCHK(hipMalloc(&c->d_heaps, (size_t)ns * c->hcap * 8ull));
   HIPCHK(hipMalloc(&c->d_gs, (size_t)ns * ncell * 4ull));
-  HIPCHK(hipMemset(c->d_gs, 0, (size_t)ns * ncell * 4ull));
+  // every initialisation goes on the context's (non-blocking) stream: a legacy
+  // hipMemset is not ordered before kernels on c->s and recycled memory leaks through
+  HIPCHK(hipMemsetAsync(c->d_gs, 0, (size_t)ns * ncell * 4ull, c->s));
   HIPCHK(hipMalloc(&c->d_epochs, (size_t)ns * 4ull));
-  HIPCHK(hipMemset(c->d_epochs, 0, (size_t)ns * 4ull));
+  HIPCHK(hipMemsetAsync(c->d_epochs, 0, (size_t)ns * 4ull, c->s));
   return TSW_OK;
 }
 
@@ -291,6 +297,43 @@ int check_err(tsw_ctx* c) {
 }
 
 // Run K3 over the queued queries until none are left (eager next hops).
+// K3 over nq queued queries (device array Q): LDS-heap kernel on small grids, with the
+// global-heap kernel for the few whose heap outgrows LDS; global-heap kernel otherwise.
+int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint8_t* res, int32_t* lens) {
+  if (nq == 0) return TSW_OK;
+  TRY(ensure_astar_scratch(c));
+  Timer t(c, CAT_ASTAR);
+  uint8_t* nh = to_tables ? c->d_nh : nullptr;
+  if (astar_lds_ok(c->G)) {
+    if (!c->d_gs16) {
+      c->nslots16 = 65536;
+      HIPCHK(hipMalloc(&c->d_gs16, (size_t)c->nslots16 * c->G.ncell * 2));
+      HIPCHK(hipMemsetAsync(c->d_gs16, 0, (size_t)c->nslots16 * c->G.ncell * 2, c->s));
+      HIPCHK(hipMalloc(&c->d_ep16, (size_t)c->nslots16 * 4));
+      HIPCHK(hipMemsetAsync(c->d_ep16, 0, (size_t)c->nslots16 * 4, c->s));
+    }
+    if (nq > c->ovf_cap) {
+      HIPCHK(hipStreamSynchronize(c->s));
+      HIPCHK(dgrow(c->d_ovf, c->ovf_cap, nq));
+    }
+    HIPCHK(hipMemsetAsync(&c->d_stat->novf, 0, 4, c->s));
+    HIPCHK(launch_astar_lds(c->G, Q, nq, nh, c->tstride, res, lens, c->d_gs16, c->d_ep16, c->nslots16, c->d_ovf,
+                            &c->d_stat->novf, c->s));
+    HIPCHK(hipMemcpyAsync(&c->h_stat->novf, &c->d_stat->novf, 4, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    const uint32_t novf = c->h_stat->novf;
+    if (novf)
+      HIPCHK(launch_astar(c->G, c->d_ovf, nullptr, novf, novf, nh, c->tstride, res, lens, c->d_heaps, c->hcap,
+                          c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
+  } else {
+    HIPCHK(launch_astar(c->G, Q, nullptr, nq, nq, nh, c->tstride, res, lens, c->d_heaps, c->hcap, c->d_gs,
+                        c->d_epochs, c->nslots, &c->d_stat->err, c->s));
+  }
+  c->st.astar_queries += nq;
+  c->st.astar_launches++;
+  return TSW_OK;
+}
+
 int resolve_all_unknown(tsw_ctx* c, const std::vector<uint32_t>& goals, const std::vector<uint32_t>& slots) {
   if (goals.empty()) return TSW_OK;
   TRY(ensure_astar_scratch(c));
@@ -307,13 +350,7 @@ int resolve_all_unknown(tsw_ctx* c, const std::vector<uint32_t>& goals, const st
     const uint32_t cnt = c->h_stat->qcount;
     if (cnt == 0) break;
     const uint32_t run = (uint32_t)std::min<size_t>(cnt, c->qcap);
-    {
-      Timer t(c, CAT_ASTAR);
-      HIPCHK(launch_astar(c->G, c->d_Q, nullptr, run, run, c->d_nh, c->tstride, nullptr, nullptr, c->d_heaps,
-                          c->hcap, c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
-    }
-    c->st.astar_queries += run;
-    c->st.astar_launches++;
+    TRY(run_astar(c, c->d_Q, run, true, nullptr, nullptr));
     TRY(check_err(c));
     if (cnt <= c->qcap) break;
   }
@@ -506,14 +543,7 @@ int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     }
     if (k.status != PLAN_NEED_QUERIES || k.qcount == 0 || k.qcount > P.qcap)
       RET(TSW_EINVAL, "plan kernel stopped without resolvable next hops");
-    TRY(ensure_astar_scratch(c));
-    {
-      Timer t(c, CAT_ASTAR);
-      HIPCHK(launch_astar(c->G, c->d_Q, nullptr, k.qcount, k.qcount, c->d_nh, c->tstride, nullptr, nullptr,
-                          c->d_heaps, c->hcap, c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
-    }
-    c->st.astar_queries += k.qcount;
-    c->st.astar_launches++;
+    TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
     TRY(check_err(c));
   }
 }
@@ -694,12 +724,13 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if ((e = hipMemcpy(c->d_goal_tab, c->h_goal_tab.data(), (size_t)ncell * 4, hipMemcpyHostToDevice)) != hipSuccess)
     return fail("copy goal_tab", e);
   if ((e = hipMalloc(&c->d_stat, sizeof(DevStatus))) != hipSuccess) return fail("malloc status", e);
-  if ((e = hipMemset(c->d_stat, 0, sizeof(DevStatus))) != hipSuccess) return fail("memset status", e);
+  if ((e = hipMemsetAsync(c->d_stat, 0, sizeof(DevStatus), c->s)) != hipSuccess) return fail("memset status", e);
   if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned status", e);
   if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
   if ((e = hipMalloc(&c->d_ticks, 8 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
-  if ((e = hipMemset(c->d_ticks, 0, 8 * sizeof(unsigned long long))) != hipSuccess) return fail("memset ticks", e);
+  if ((e = hipMemsetAsync(c->d_ticks, 0, 8 * sizeof(unsigned long long), c->s)) != hipSuccess)
+    return fail("memset ticks", e);
   hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, c->device);
   if (c->wall_khz <= 0) c->wall_khz = 100000;
   if ((e = hipHostMalloc(&c->h_ctl, sizeof(PlanCtl), hipHostMallocDefault)) != hipSuccess)
@@ -708,6 +739,7 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   size_t freeb = 0, totalb = 0;
   hipMemGetInfo(&freeb, &totalb);
   c->table_budget = (opts && opts->table_budget_bytes) ? opts->table_budget_bytes : (uint64_t)(freeb / 2);
+  if ((e = hipStreamSynchronize(c->s)) != hipSuccess) return fail("stream sync", e);
   return c;
 }
 
@@ -720,6 +752,7 @@ void tsw_destroy(tsw_ctx* c) {
   };
   fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
+  fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
   fre(c->d_gt); fre(c->d_dec); fre(c->d_mu); fre(c->d_dups); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
   if (c->h_dups) (void)hipHostFree(c->h_dups);
@@ -807,13 +840,7 @@ int tsw_get_path_next(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, u
   TRY(ensure_queue(c, q.size()));
   TRY(ensure_res(c, k));
   HIPCHK(hipMemcpyAsync(c->d_Q, q.data(), q.size() * sizeof(AstarQuery), hipMemcpyHostToDevice, c->s));
-  {
-    Timer t(c, CAT_ASTAR);
-    HIPCHK(launch_astar(c->G, c->d_Q, nullptr, (uint32_t)q.size(), (uint32_t)q.size(), nullptr, 0, c->d_res,
-                        c->d_lens, c->d_heaps, c->hcap, c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
-  }
-  c->st.astar_queries += q.size();
-  c->st.astar_launches++;
+  TRY(run_astar(c, c->d_Q, (uint32_t)q.size(), false, c->d_res, c->d_lens));
   std::vector<uint8_t> res(k);
   std::vector<int32_t> lens(k);
   HIPCHK(hipMemcpyAsync(res.data(), c->d_res, k, hipMemcpyDeviceToHost, c->s));
@@ -939,6 +966,26 @@ int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, cons
   return TSW_OK;
 }
 
+int tsw_next_hop_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* out) {
+  if (!c) return TSW_EINVAL;
+  if (k == 0) return TSW_OK;
+  if (!goals || !out) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  std::vector<uint32_t> gv(goals, goals + k);
+  for (uint32_t g : gv)
+    if (!cell_id_ok(c, g)) RET(TSW_EINVAL, "goal cell off-grid or blocked");
+  TRY(ensure_tables(c, gv));
+  const size_t ncell = c->G.ncell;
+  for (uint32_t i = 0; i < k; ++i) {
+    const int32_t slot = c->h_goal_tab[gv[i]];
+    HIPCHK(hipMemcpyAsync(out + (size_t)i * ncell, c->d_nh + (size_t)slot * c->tstride, ncell,
+                          hipMemcpyDeviceToHost, c->s));
+  }
+  HIPCHK(hipStreamSynchronize(c->s));
+  resolve_timing(c);
+  return TSW_OK;
+}
+
 int tsw_clear_tables(tsw_ctx* c) {
   if (!c) return TSW_EINVAL;
   TRY(set_device(c));
@@ -969,7 +1016,7 @@ int tsw_reset_stats(tsw_ctx* c) {
   const uint64_t tabs = c->st.tables;
   c->st = tsw_stats{};
   c->st.tables = tabs;
-  if (c->d_ticks) (void)hipMemset(c->d_ticks, 0, 8 * sizeof(unsigned long long));
+  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 8 * sizeof(unsigned long long), c->s);
   return TSW_OK;
 }
 

@@ -150,3 +150,52 @@ def test_mapd_more(name, n, m, seed, flags):
         t = int(np.argmax((goal != rgoal).any(axis=0)))
         pytest.fail(f"goal divergence first at t={t}")
     assert np.array_equal(rec, ref)
+
+
+@pytest.mark.parametrize("name,flags,ngoals", [("rand32", TSW_F_EAGER_NEXTHOP, 0), ("rand16", TSW_F_EAGER_NEXTHOP, 0),
+                                               ("open8", TSW_F_EAGER_NEXTHOP, 0)])
+def test_next_hop_tables_all_pairs(name, flags, ngoals):
+    """Every (cell, goal) next hop of the eager tables == get_path(cell, goal)[1] (exhaustive)."""
+    rows = _grid(name)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@")).astype(np.uint32)
+    goals = free if ngoals == 0 else free[:ngoals]
+    with Planner(rows, flags=flags) as p:
+        tabs = p.next_hop_tables(goals)
+    bad = []
+    for k, g in enumerate(goals):
+        ref = og.next_codes(int(g))
+        got = tabs[k]
+        mism = np.flatnonzero((got != ref) & (ref != 0xFF))
+        if mism.size:
+            bad.append((int(g), int(mism[0]), int(got[mism[0]]), int(ref[mism[0]]), int(mism.size)))
+    assert not bad, f"{len(bad)} goals with mismatching next hops, first {bad[:4]}"
+
+
+@pytest.mark.parametrize("name,n,seed", [("rand32", 200, 2), ("rand32", 300, 5), ("bundled", 400, 6)])
+def test_step_deterministic_and_exact(name, n, seed):
+    """Repeated identical tsw_step calls (fresh contexts) give identical results == oracle."""
+    rows = _grid(name)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    comp = maps.largest_component(rows)
+    rng = np.random.default_rng(seed)
+    cellid = np.array([y * cells.shape[1] + x for (x, y) in comp], dtype=np.uint32)
+    v = cellid[rng.choice(len(comp), size=n, replace=False)]
+    g = cellid[rng.choice(len(comp), size=n, replace=True)]
+    g[: n // 4] = v[: n // 4]
+    outs = []
+    for rep in range(3):
+        with Planner(rows) as p:
+            vv, gg = v.copy(), g.copy()
+            for _ in range(4):
+                vv, gg = p.step(vv, gg)
+            outs.append((vv, gg))
+    rv, rg = v.copy(), g.copy()
+    for _ in range(4):
+        rv, rg = og.step(rv, rg)
+    for rep, (vv, gg) in enumerate(outs):
+        dv = np.flatnonzero(vv != rv)
+        dg = np.flatnonzero(gg != rg)
+        assert dv.size == 0 and dg.size == 0, f"rep {rep}: v differs at {dv[:8]}, g differs at {dg[:8]}"

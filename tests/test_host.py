@@ -1,0 +1,79 @@
+"""CPU: host-side logic — the C ABI library loads and exports every declared symbol,
+fails loudly without a GPU, map generators are deterministic, MovingAI I/O round-trips."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import p2p_distributed_tswap_amd as pkg
+from p2p_distributed_tswap_amd import maps
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    txt = open(os.path.join(ROOT, "include", "tswap.h")).read()
+    return sorted(set(re.findall(r"\b(tsw_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_and_package_agree():
+    assert set(_declared()) == set(pkg.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_symbol():
+    if not os.path.exists(pkg.LIB_PATH):
+        pytest.skip("libtswap_hip.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(pkg.LIB_PATH)
+    for sym in _declared():
+        assert hasattr(lib, sym), sym
+
+
+def test_no_cpu_fallback_without_gpu():
+    """The product path refuses to run when no HIP device is visible."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    if not os.path.exists(pkg.LIB_PATH):
+        pytest.skip("libtswap_hip.so not built")
+    with pytest.raises(pkg.TswapError):
+        pkg.Planner(maps.open_map(4, 4))
+
+
+def test_missing_library_raises(tmp_path):
+    with pytest.raises(pkg.TswapError):
+        pkg._lib = None
+        pkg.load_library(str(tmp_path / "nope.so"))
+
+
+def test_grid_to_bytes_ragged():
+    with pytest.raises(pkg.TswapError):
+        pkg.grid_to_bytes(["...", ".."])
+
+
+def test_generators_deterministic():
+    a = maps.random_map(32, 32, 0.2, 0x3232)
+    assert a == maps.random_map(32, 32, 0.2, 0x3232)
+    s1, t1 = maps.make_instance(a, 50, 100, 9)
+    s2, t2 = maps.make_instance(a, 50, 100, 9)
+    assert np.array_equal(s1, s2) and np.array_equal(t1, t2)
+    comp = set(maps.largest_component(a))
+    assert all(tuple(p) in comp for p in s1.tolist())
+    assert all((t[0], t[1]) in comp and (t[2], t[3]) in comp for t in t1.tolist())
+    assert len({tuple(p) for p in s1.tolist()}) == 50  # distinct starts
+    assert all((t[0], t[1]) != (t[2], t[3]) for t in t1.tolist())
+
+
+def test_config_maps_shapes():
+    w = maps.warehouse_map()
+    assert len(w) == 84 and len(w[0]) == 170
+    assert len(maps.bundled_map()) == 100 and set("".join(maps.bundled_map())) == {"."}
+
+
+def test_movingai_roundtrip(tmp_path):
+    rows = maps.random_map(12, 7, 0.3, 5)
+    p = tmp_path / "m.map"
+    maps.write_movingai(str(p), rows)
+    assert maps.read_movingai(str(p)) == rows
