@@ -45,7 +45,28 @@ def parse():
     ap.add_argument("--bfs-goals", type=int, default=10000)
     ap.add_argument("--bfs-reps", type=int, default=3)
     ap.add_argument("--config", default="c2_random_32_32_20")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, default) or gloo (rehearsing N ranks on one GPU)")
     return ap.parse_args()
+
+
+def profiled_traffic(kernel_prefix: str):
+    """Per-launch HBM bytes of a kernel from the newest committed PMC summary
+    (profiles/<round>/summary.json, made by scripts/profile_round.sh + summarize_profile.py:
+    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction)."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")), key=os.path.getmtime)
+    for p in reversed(paths):
+        try:
+            with open(p) as f:
+                ks = json.load(f)["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        for name, d in ks.items():
+            if name.startswith(kernel_prefix) and "hbm_bytes_per_launch" in d:
+                return float(d["hbm_bytes_per_launch"]), os.path.relpath(p, ROOT)
+    return None, None
 
 
 def bfs_bytes_per_goal(w: int, h: int, with_nh: bool) -> int:
@@ -63,10 +84,14 @@ def main():
     import torch
 
     dist = None
+    dev = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from p2p_distributed_tswap_amd import Planner, maps
 
@@ -93,7 +118,7 @@ def main():
     rows = fac()
     h, w = len(rows), len(rows[0])
     starts, tasks = maps.make_instance(rows, n_agents, n_tasks, seed + rank)
-    planner = Planner(rows, device=local if world > 1 else 0)
+    planner = Planner(rows, device=dev)
 
     def one_plan():
         planner.clear_tables()
@@ -121,8 +146,7 @@ def main():
     # dominant kernel inside the timed region (device time from HIP events)
     cats = {
         "k_astar (K3 exact A* next hop)": (st["astar_ms"], st["astar_launches"]),
-        "k_walk (K2 serial tswap_step commit)": (st["walker_ms"], st["walker_launches"]),
-        "k_assign (K4 task assignment)": (st["assign_ms"], st["assign_launches"]),
+        "k_plan (K2 tswap_step + K4 assignment, persistent)": (st["walker_ms"], st["walker_launches"]),
         "k_bfs (K1 BFS tables + next-hop codes)": (st["bfs_ms"], st["bfs_launches"]),
     }
     dom = max(cats, key=lambda k: cats[k][0])
@@ -136,6 +160,7 @@ def main():
         # agent-steps covered by one launch of that kernel
         per_launch_bytes = 46.0 * n_agents * steps_total / max(dom_launches, 1)
     achieved = per_launch_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    traffic, traffic_src = profiled_traffic(dom.split()[0])
     roofline = {
         "kernel": dom,
         "bound": "hbm",
@@ -143,7 +168,8 @@ def main():
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 6),
-        "traffic": None,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
         "avg_launch_us": round(avg_launch_ms * 1e3, 3),
         "launches": int(dom_launches),
         "algorithmic_bytes_per_launch": round(per_launch_bytes, 1),
@@ -159,7 +185,7 @@ def main():
         rng = np.random.default_rng(0x520D)
         goals = np.sort(rng.choice(free, size=min(args.bfs_goals, free.size), replace=False)).astype(np.uint32)
         mine = goals[rank::world]
-        cp = Planner(crow, device=local if world > 1 else 0)
+        cp = Planner(crow, device=dev)
         ncell = 256 * 257
         out = torch.empty((mine.size, ncell), dtype=torch.int16, device="cuda")
         cp.dist_tables_device(mine, out.data_ptr())  # warm-up
@@ -175,17 +201,21 @@ def main():
         bytes_goal = bfs_bytes_per_goal(256, 257, False)
         gather_ms = None
         if dist is not None:
-            # RCCL all-gather of the goal-sharded tables over xGMI (north_star)
-            per = (goals.size + world - 1) // world
-            pad = torch.zeros((per, ncell), dtype=torch.int16, device="cuda")
-            pad[: mine.size].copy_(out)
-            full = torch.empty((world * per, ncell), dtype=torch.int16, device="cuda")
+            # goal-sharded K1 + RCCL all-gather over xGMI (north_star), then every rank ingests
+            # every table into its table store (sharding.py)
+            from p2p_distributed_tswap_amd import sharding
+
+            build = lambda g, o: cp.dist_tables_device(g, o.data_ptr())  # noqa: E731
             barrier()
             tg = time.perf_counter()
-            dist.all_gather_into_tensor(full, pad)
+            full = sharding.build_and_allgather(goals, ncell, rank, world, build, dist, "cuda")
             barrier()
             gather_ms = allmax(time.perf_counter() - tg) * 1e3
-            del full, pad
+            torch.cuda.synchronize()
+            for _, gl, off in sharding.gathered_blocks(goals, world):
+                if gl.size:
+                    cp.import_tables_device(gl, full[off:off + gl.size].data_ptr())
+            del full
         cells_per_s = allsum(float(mine.size * ncell)) * args.bfs_reps / tbw
         k_gbs = mine.size * bytes_goal / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
         bfs = {
@@ -197,7 +227,8 @@ def main():
             "kernel_GBps": round(k_gbs, 2),
             "hbm_frac": round(k_gbs / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_goal": bytes_goal,
-            "allgather_ms": round(gather_ms, 3) if gather_ms is not None else None,
+            # N > 1: wall time of (this rank's K1 shard + RCCL all-gather of all tables), max over ranks
+            "sharded_build_allgather_ms": round(gather_ms, 3) if gather_ms is not None else None,
         }
         del out
         cp.close()
