@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -34,6 +35,7 @@ struct DevStatus {
   uint32_t done;
   uint32_t qcount;
   uint32_t novf;  // LDS A*: queries handed to the global-heap kernel
+  uint32_t work;  // k_bfs_wave goal dequeue counter
 };
 
 enum { CAT_BFS = 0, CAT_ASTAR = 1, CAT_WALK = 2, CAT_ASSIGN = 3, NCAT = 4 };
@@ -50,6 +52,13 @@ struct tsw_ctx {
   uint8_t* d_nbmask = nullptr;
   uint32_t* d_freebits = nullptr;
   int max_lds = 65536, num_cu = 256;
+  // K1 v2 (k_bfs_wave) padded grid + per-wave scratch
+  uint32_t Wp = 0, npw = 0, nfw = 0, nanch = 0, bfs_cap = 512, bfs_mode = 0;  // mode 0 auto, 1 wave, 2 block
+  uint32_t* d_frp = nullptr;
+  uint32_t* d_rb = nullptr;
+  uint32_t* d_anch = nullptr;
+  uint16_t* d_lovf = nullptr;
+  uint64_t wave_scratch = 0;
 
   // goal-table store
   uint64_t tstride = 0;
@@ -363,6 +372,63 @@ bool eager_policy(const tsw_ctx* c, size_t new_tables) {
   return c->G.ncell <= 4096 && (uint64_t)new_tables * c->G.ncell <= (8ull << 20);
 }
 
+// K1 over k goals (device arrays; slots may be null = goal index): the wave-per-goal kernel
+// when its LDS fits, else the workgroup-per-goal kernel. Next-hop codes (nh != null) come
+// fused from k_bfs, or from k_classify over the finished tables after k_bfs_wave.
+int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k, uint16_t* dist, uint64_t dstride,
+            uint8_t* nh) {
+  if (k == 0) return TSW_OK;
+  uint32_t nwv = 0;
+  if (c->bfs_mode != 2 && c->npw <= 0x8000u)
+    nwv = bfs_wave_waves_per_block(c->npw, c->nfw, c->bfs_cap, c->max_lds);
+  if (nwv == 0 && c->bfs_mode == 1) RET(TSW_EINVAL, "k_bfs_wave does not fit this grid (TSW_BFS_KERNEL=wave)");
+  Timer t(c, CAT_BFS);
+  if (nwv == 0) {
+    HIPCHK(launch_bfs(c->G, goals, slots, k, dist, dstride, nh, dstride, &c->d_stat->err, c->max_lds, c->num_cu,
+                      c->s));
+    return TSW_OK;
+  }
+  const uint64_t want = (uint64_t)c->num_cu * nwv;
+  if (want > c->wave_scratch) {
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (c->d_anch) HIPCHK(hipFree(c->d_anch));
+    if (c->d_lovf) HIPCHK(hipFree(c->d_lovf));
+    c->d_anch = nullptr;
+    c->d_lovf = nullptr;
+    c->wave_scratch = 0;
+    HIPCHK(hipMalloc(&c->d_anch, (size_t)want * std::max<uint32_t>(c->nanch, 1u) * 4u));
+    HIPCHK(hipMalloc(&c->d_lovf, (size_t)want * 2u * c->npw * 2u));
+    c->wave_scratch = want;
+  }
+  WaveBfsArgs A{};
+  A.W = c->G.W;
+  A.H = c->G.H;
+  A.Ww = c->G.Ww;
+  A.Wp = c->Wp;
+  A.npw = c->npw;
+  A.nfw = c->nfw;
+  A.nanch = std::max<uint32_t>(c->nanch, 1u);
+  A.cap = c->bfs_cap;
+  A.frp = c->d_frp;
+  A.rb = c->d_rb;
+  A.goals = goals;
+  A.slots = slots;
+  A.k = k;
+  A.dist = dist;
+  A.dstride = dstride;
+  A.anch = c->d_anch;
+  A.lovf = c->d_lovf;
+  A.work = &c->d_stat->work;
+  A.err = &c->d_stat->err;
+  A.vec16 = (c->G.W % 8u == 0u && dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u) ? 1u : 0u;
+  A.max_waves = 16;
+  A.scratch_waves = c->wave_scratch;
+  HIPCHK(hipMemsetAsync(&c->d_stat->work, 0, 4, c->s));
+  HIPCHK(launch_bfs_wave(A, c->max_lds, c->num_cu, c->s));
+  if (nh) HIPCHK(launch_classify(c->G, goals, slots, k, dist, dstride, nh, c->s));
+  return TSW_OK;
+}
+
 // Make sure every goal in `goals` (valid free cells) has a table.
 int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
   std::vector<uint32_t> newg;
@@ -410,11 +476,7 @@ int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
   TRY(ensure_tmp(c, newg.size()));
   HIPCHK(hipMemcpyAsync(c->d_tmp_a, newg.data(), newg.size() * 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
-  {
-    Timer t(c, CAT_BFS);
-    HIPCHK(launch_bfs(c->G, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh,
-                      c->tstride, &c->d_stat->err, c->max_lds, c->num_cu, c->s));
-  }
+  TRY(run_bfs(c, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh));
   c->st.bfs_goals += newg.size();
   c->st.bfs_launches++;
   HIPCHK(hipMemcpyAsync(c->d_goal_tab, c->h_goal_tab.data(), (size_t)c->G.ncell * 4, hipMemcpyHostToDevice, c->s));
@@ -719,6 +781,32 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
     return fail("copy freebits", e);
   c->G.nbmask = c->d_nbmask;
   c->G.freebits = c->d_freebits;
+  {
+    // k_bfs_wave layout: word (r, cw) at (r + 1) * Wp + cw, zero guard column and rows;
+    // rb[p] = number of run starts (free cell whose west is blocked, or bit 0 of a word)
+    // in padded words before p = index of p's first anchor
+    c->Wp = Ww + 1u;
+    c->npw = (h + 2u) * c->Wp;
+    c->nfw = (c->npw + 31u) / 32u;
+    std::vector<uint32_t> frp(c->npw, 0u), rb(c->npw, 0u);
+    for (uint32_t y = 0; y < h; ++y)
+      for (uint32_t cw = 0; cw < Ww; ++cw) frp[(size_t)(y + 1u) * c->Wp + cw] = fb[(size_t)y * Ww + cw];
+    uint32_t acc = 0;
+    for (uint32_t p = 0; p < c->npw; ++p) {
+      rb[p] = acc;
+      const uint32_t f = frp[p];
+      acc += (uint32_t)__builtin_popcount(f & ~(f << 1));
+    }
+    c->nanch = acc;
+    if ((e = hipMalloc(&c->d_frp, (size_t)c->npw * 4)) != hipSuccess) return fail("malloc frp", e);
+    if ((e = hipMemcpy(c->d_frp, frp.data(), (size_t)c->npw * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      return fail("copy frp", e);
+    if ((e = hipMalloc(&c->d_rb, (size_t)c->npw * 4)) != hipSuccess) return fail("malloc rb", e);
+    if ((e = hipMemcpy(c->d_rb, rb.data(), (size_t)c->npw * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      return fail("copy rb", e);
+    if (const char* m = getenv("TSW_BFS_KERNEL")) c->bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : 0u;
+    if (const char* m = getenv("TSW_BFS_LISTCAP")) c->bfs_cap = std::max(1, std::min(atoi(m), 32768));
+  }
   c->h_goal_tab.assign(ncell, -1);
   if ((e = hipMalloc(&c->d_goal_tab, (size_t)ncell * 4)) != hipSuccess) return fail("malloc goal_tab", e);
   if ((e = hipMemcpy(c->d_goal_tab, c->h_goal_tab.data(), (size_t)ncell * 4, hipMemcpyHostToDevice)) != hipSuccess)
@@ -750,7 +838,7 @@ void tsw_destroy(tsw_ctx* c) {
   auto fre = [](void* p) {
     if (p) (void)hipFree(p);
   };
-  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
+  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_rb); fre(c->d_anch); fre(c->d_lovf); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
   fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
@@ -892,11 +980,7 @@ int tsw_dist_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16
     if (!cell_id_ok(c, goals[i])) RET(TSW_EINVAL, "goal cell off-grid or blocked");
   TRY(ensure_tmp(c, k));
   HIPCHK(hipMemcpyAsync(c->d_tmp_a, goals, (size_t)k * 4, hipMemcpyHostToDevice, c->s));
-  {
-    Timer t(c, CAT_BFS);
-    HIPCHK(launch_bfs(c->G, c->d_tmp_a, nullptr, k, dev_out, c->G.ncell, nullptr, 0, &c->d_stat->err, c->max_lds,
-                      c->num_cu, c->s));
-  }
+  TRY(run_bfs(c, c->d_tmp_a, nullptr, k, dev_out, c->G.ncell, nullptr));
   c->st.bfs_goals += k;
   c->st.bfs_launches++;
   TRY(check_err(c));

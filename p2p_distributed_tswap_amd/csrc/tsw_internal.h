@@ -64,5 +64,6 @@ constexpr uint32_t ERR_DIST_OVERFLOW = 2u;
 constexpr uint32_t ERR_G_OVERFLOW = 4u;
 constexpr uint32_t ERR_NO_TABLE = 8u;
 constexpr uint32_t ERR_WALK_OVERFLOW = 16u;
+constexpr uint32_t ERR_BFS_LIST = 32u;     // k_bfs_wave: a queued word gained no cell (logic error)
 
 }  // namespace tsw

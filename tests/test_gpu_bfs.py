@@ -1,0 +1,143 @@
+"""K1 parity: both BFS kernels (k_bfs_wave: one wavefront per goal; k_bfs: one workgroup per
+goal) against the oracle's BFS (oracle/tswap_oracle.c, cross-checked against A* path lengths in
+test_oracle.py), bit-exact, on ragged widths, list-overflow paths and the full-size den520d-like
+cave (BASELINE configs[3])."""
+import os
+
+import numpy as np
+import pytest
+
+from p2p_distributed_tswap_amd import Planner, maps
+from oracle import OracleGraph
+
+pytestmark = pytest.mark.gpu
+
+
+class _env:
+    """Kernel selection is read when a context is created (TSW_BFS_KERNEL, TSW_BFS_LISTCAP)."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update({k: str(v) for k, v in self.kv.items()})
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+GRIDS = {
+    "open8": lambda: maps.open_map(8, 8),
+    "line1x40": lambda: maps.open_map(1, 40),
+    "row40x1": lambda: maps.open_map(40, 1),
+    "rand33x17": lambda: maps.random_map(33, 17, 0.25, 11),
+    "rand32": lambda: maps.random_map(32, 32, 0.20, 0x3232),
+    "rand100x31": lambda: maps.random_map(100, 31, 0.35, 5),
+    "warehouse": lambda: maps.warehouse_map(170, 84, 0x170084),
+    "cave64": lambda: maps.cave_map(64, 65, 3),
+    "bundled": maps.bundled_map,
+}
+
+
+def _check(rows, goals, **env):
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    with _env(**env), Planner(rows) as p:
+        got = p.dist_tables(goals)
+    for k, g in enumerate(goals):
+        ref = og.bfs(int(g))
+        assert np.array_equal(got[k], ref), f"goal {g}: {np.count_nonzero(got[k] != ref)} cells differ"
+
+
+def _goals(rows, n, seed):
+    cells = maps.rows_to_array(rows)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@"))
+    rng = np.random.default_rng(seed)
+    return rng.choice(free, size=min(n, free.size), replace=False).astype(np.uint32)
+
+
+@pytest.mark.parametrize("kernel", ["wave", "block"])
+@pytest.mark.parametrize("name", sorted(GRIDS))
+def test_bfs_kernels_bit_exact(kernel, name):
+    rows = GRIDS[name]()
+    _check(rows, _goals(rows, 40, 7), TSW_BFS_KERNEL=kernel)
+
+
+@pytest.mark.parametrize("cap", [1, 3, 17])
+def test_bfs_wave_list_overflow(cap):
+    """Lists longer than the LDS capacity spill to the per-wave global overflow area."""
+    rows = maps.cave_map(128, 97, 9)
+    _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="wave", TSW_BFS_LISTCAP=cap)
+
+
+def test_bfs_wave_unreachable_pockets():
+    """Walled-off pockets stay 0xFFFF; goals inside a pocket see only the pocket."""
+    a = np.zeros((40, 70), dtype=bool)
+    a[10, :] = True          # full wall: two halves
+    a[20:25, 30:35] = True   # closed box ...
+    a[21:24, 31:34] = False  # ... with a hollow pocket
+    rows = maps.to_rows(a)
+    cells = maps.rows_to_array(rows)
+    goals = np.array([0, 69, 11 * 70 + 5, 22 * 70 + 32, 39 * 70 + 69], dtype=np.uint32)
+    assert all(cells.reshape(-1)[g] != ord("@") for g in goals)
+    _check(rows, goals, TSW_BFS_KERNEL="wave")
+
+
+class _DevBuf:
+    """Device buffer from the HIP runtime the library itself links (/opt/rocm), not torch's
+    bundled one: a second runtime in the process cannot open the device after the first."""
+
+    def __init__(self, nbytes):
+        import ctypes
+
+        self.ct = ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.ptr = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(self.ptr), ctypes.c_size_t(nbytes)) == 0
+        self.nbytes = nbytes
+
+    def to_host(self, arr):
+        assert self.hip.hipDeviceSynchronize() == 0
+        assert self.hip.hipMemcpy(arr.ctypes.data_as(self.ct.c_void_p), self.ptr,
+                                  self.ct.c_size_t(arr.nbytes), 2) == 0  # hipMemcpyDeviceToHost
+        return arr
+
+    def __del__(self):
+        self.hip.hipFree(self.ptr)
+
+
+def test_bfs_wave_den520d_full_size():
+    """BASELINE configs[3] geometry: 256x257 cave, 1,000 distinct goals through the device-output
+    entry point the bench times (16-B stores), every table bit-exact vs the oracle."""
+    rows = maps.cave_map(256, 257, 0x520D)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    goals = np.sort(_goals(rows, 1000, 0x520D))
+    ncell = 256 * 257
+    with _env(TSW_BFS_KERNEL="wave"), Planner(rows) as p:
+        buf = _DevBuf(goals.size * ncell * 2)
+        p.dist_tables_device(goals, buf.ptr.value)
+        got = buf.to_host(np.empty((goals.size, ncell), dtype=np.uint16))
+    for k, g in enumerate(goals):
+        ref = og.bfs(int(g))
+        assert np.array_equal(got[k], ref), f"goal {g}: {np.count_nonzero(got[k] != ref)} cells differ"
+
+
+def test_bfs_wave_symmetry_full_goal_set():
+    """Size-independent property at full size: d_g(c) == d_c(g) for every pair of goals, over all
+    free cells of a 96x97 cave used as goals (the table matrix restricted to goals is symmetric),
+    and blocked cells are 0xFFFF in every table."""
+    rows = maps.cave_map(96, 97, 0x5EED)
+    cells = maps.rows_to_array(rows).reshape(-1)
+    free = np.flatnonzero(cells != ord("@")).astype(np.uint32)
+    with _env(TSW_BFS_KERNEL="wave"), Planner(rows) as p:
+        t = p.dist_tables(free)
+    sub = t[:, free].astype(np.int64)
+    assert np.array_equal(sub, sub.T)
+    assert np.all(t[:, cells == ord("@")] == 0xFFFF)
+    assert np.all(t[np.arange(free.size), free] == 0)
