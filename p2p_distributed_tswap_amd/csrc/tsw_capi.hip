@@ -53,12 +53,12 @@ struct tsw_ctx {
   uint32_t* d_freebits = nullptr;
   int max_lds = 65536, num_cu = 256;
   // K1 v2 (k_bfs_wave) padded grid + per-wave scratch
-  uint32_t Wp = 0, npw = 0, nfw = 0, nanch = 0, bfs_cap = 512, bfs_mode = 0;  // mode 0 auto, 1 wave, 2 block
+  uint32_t Wp = 0, npw = 0, bfs_cap = 512, bfs_mode = 0;  // mode 0 auto, 1 wave, 2 block
   uint32_t* d_frp = nullptr;
-  uint32_t* d_rb = nullptr;
-  uint32_t* d_anch = nullptr;
+  uint16_t* d_anch = nullptr;
   uint16_t* d_lovf = nullptr;
   uint64_t wave_scratch = 0;
+  unsigned long long* d_bprof = nullptr;  // TSW_BFS_PROF=1: k_bfs_wave cycle split, printed per launch
 
   // goal-table store
   uint64_t tstride = 0;
@@ -380,7 +380,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   if (k == 0) return TSW_OK;
   uint32_t nwv = 0;
   if (c->bfs_mode != 2 && c->npw <= 0x8000u)
-    nwv = bfs_wave_waves_per_block(c->npw, c->nfw, c->bfs_cap, c->max_lds);
+    nwv = bfs_wave_waves_per_block(c->npw, c->bfs_cap, c->max_lds);
   if (nwv == 0 && c->bfs_mode == 1) RET(TSW_EINVAL, "k_bfs_wave does not fit this grid (TSW_BFS_KERNEL=wave)");
   Timer t(c, CAT_BFS);
   if (nwv == 0) {
@@ -396,7 +396,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     c->d_anch = nullptr;
     c->d_lovf = nullptr;
     c->wave_scratch = 0;
-    HIPCHK(hipMalloc(&c->d_anch, (size_t)want * std::max<uint32_t>(c->nanch, 1u) * 4u));
+    HIPCHK(hipMalloc(&c->d_anch, (size_t)want * c->npw * 32u * 2u));
     HIPCHK(hipMalloc(&c->d_lovf, (size_t)want * 2u * c->npw * 2u));
     c->wave_scratch = want;
   }
@@ -406,11 +406,8 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   A.Ww = c->G.Ww;
   A.Wp = c->Wp;
   A.npw = c->npw;
-  A.nfw = c->nfw;
-  A.nanch = std::max<uint32_t>(c->nanch, 1u);
   A.cap = c->bfs_cap;
   A.frp = c->d_frp;
-  A.rb = c->d_rb;
   A.goals = goals;
   A.slots = slots;
   A.k = k;
@@ -421,10 +418,23 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   A.work = &c->d_stat->work;
   A.err = &c->d_stat->err;
   A.vec16 = (c->G.W % 8u == 0u && dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u) ? 1u : 0u;
-  A.max_waves = 16;
+  A.max_waves = getenv("TSW_BFS_WAVES") ? (uint32_t)std::max(1, atoi(getenv("TSW_BFS_WAVES"))) : 16u;
   A.scratch_waves = c->wave_scratch;
+  A.prof = nullptr;
+  if (getenv("TSW_BFS_PROF")) {
+    if (!c->d_bprof) HIPCHK(hipMalloc(&c->d_bprof, 4 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(c->d_bprof, 0, 4 * sizeof(unsigned long long), c->s));
+    A.prof = (uint64_t*)c->d_bprof;
+  }
   HIPCHK(hipMemsetAsync(&c->d_stat->work, 0, 4, c->s));
   HIPCHK(launch_bfs_wave(A, c->max_lds, c->num_cu, c->s));
+  if (A.prof) {
+    unsigned long long h[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(h, c->d_bprof, sizeof h, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    fprintf(stderr, "[k_bfs_wave] goals %u  bfs %.0f cyc/goal  decode %.0f cyc/goal  levels %.1f/goal  chunks %.1f/goal\n",
+            k, (double)h[0] / k, (double)h[1] / k, (double)h[2] / k, (double)h[3] / k);
+  }
   if (nh) HIPCHK(launch_classify(c->G, goals, slots, k, dist, dstride, nh, c->s));
   return TSW_OK;
 }
@@ -782,28 +792,15 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   c->G.nbmask = c->d_nbmask;
   c->G.freebits = c->d_freebits;
   {
-    // k_bfs_wave layout: word (r, cw) at (r + 1) * Wp + cw, zero guard column and rows;
-    // rb[p] = number of run starts (free cell whose west is blocked, or bit 0 of a word)
-    // in padded words before p = index of p's first anchor
+    // k_bfs_wave layout: word (r, cw) at (r + 1) * Wp + cw, zero guard column and rows
     c->Wp = Ww + 1u;
     c->npw = (h + 2u) * c->Wp;
-    c->nfw = (c->npw + 31u) / 32u;
-    std::vector<uint32_t> frp(c->npw, 0u), rb(c->npw, 0u);
+    std::vector<uint32_t> frp(c->npw, 0u);
     for (uint32_t y = 0; y < h; ++y)
       for (uint32_t cw = 0; cw < Ww; ++cw) frp[(size_t)(y + 1u) * c->Wp + cw] = fb[(size_t)y * Ww + cw];
-    uint32_t acc = 0;
-    for (uint32_t p = 0; p < c->npw; ++p) {
-      rb[p] = acc;
-      const uint32_t f = frp[p];
-      acc += (uint32_t)__builtin_popcount(f & ~(f << 1));
-    }
-    c->nanch = acc;
     if ((e = hipMalloc(&c->d_frp, (size_t)c->npw * 4)) != hipSuccess) return fail("malloc frp", e);
     if ((e = hipMemcpy(c->d_frp, frp.data(), (size_t)c->npw * 4, hipMemcpyHostToDevice)) != hipSuccess)
       return fail("copy frp", e);
-    if ((e = hipMalloc(&c->d_rb, (size_t)c->npw * 4)) != hipSuccess) return fail("malloc rb", e);
-    if ((e = hipMemcpy(c->d_rb, rb.data(), (size_t)c->npw * 4, hipMemcpyHostToDevice)) != hipSuccess)
-      return fail("copy rb", e);
     if (const char* m = getenv("TSW_BFS_KERNEL")) c->bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : 0u;
     if (const char* m = getenv("TSW_BFS_LISTCAP")) c->bfs_cap = std::max(1, std::min(atoi(m), 32768));
   }
@@ -838,7 +835,7 @@ void tsw_destroy(tsw_ctx* c) {
   auto fre = [](void* p) {
     if (p) (void)hipFree(p);
   };
-  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_rb); fre(c->d_anch); fre(c->d_lovf); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
+  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_anch); fre(c->d_lovf); fre(c->d_bprof); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
   fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);

@@ -18,24 +18,24 @@ hipError_t launch_bfs(const DevGrid& G, const uint32_t* goals, const uint32_t* s
 // K1 v2 (tsw_bfs.hip): one wavefront per goal. Padded layout: word (r, c) of the W x H grid
 // sits at p = (r + 1) * Wp + c, Wp = Ww + 1 (zero guard word per row, zero guard rows).
 struct WaveBfsArgs {
-  uint32_t W, H, Ww, Wp, npw, nfw, nanch, cap;
+  uint32_t W, H, Ww, Wp, npw, cap, klog;
   const uint32_t* frp;    // [npw] padded free-cell bitmap
-  const uint32_t* rb;     // [npw] index of the first run-start anchor of each padded word
   const uint32_t* goals;
   const uint32_t* slots;  // table slot per goal (nullptr: slot = goal index)
   uint32_t k;
   uint16_t* dist;
   uint64_t dstride;
-  uint32_t* anch;         // per-wave anchor scratch, nanch u32 each
+  uint16_t* anch;         // per-wave anchor scratch, npw * 32 u16 each (cell-indexed)
   uint16_t* lovf;         // per-wave list overflow, 2 * npw u16 each
   uint32_t* work;         // goal dequeue counter (zeroed before the launch)
   uint32_t* err;
   uint32_t vec16;         // 16-B stores allowed (W % 8 == 0, 16-B aligned tables)
   uint32_t max_waves;     // waves per workgroup cap
   uint64_t scratch_waves; // waves the scratch buffers are sized for
+  uint64_t* prof;         // optional: [bfs cycles, decode cycles, levels, chunks] summed over waves
 };
-size_t bfs_wave_lds_one(uint32_t npw, uint32_t nfw, uint32_t cap);
-uint32_t bfs_wave_waves_per_block(uint32_t npw, uint32_t nfw, uint32_t cap, int max_lds);
+// waves per workgroup that fit max_lds (0: the kernel does not fit this grid)
+uint32_t bfs_wave_waves_per_block(uint32_t npw, uint32_t cap, int max_lds);
 hipError_t launch_bfs_wave(const WaveBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
 
 hipError_t launch_classify(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,

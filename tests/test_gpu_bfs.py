@@ -41,6 +41,9 @@ GRIDS = {
     "warehouse": lambda: maps.warehouse_map(170, 84, 0x170084),
     "cave64": lambda: maps.cave_map(64, 65, 3),
     "bundled": maps.bundled_map,
+    # isolated free cells at odd x: 16 run starts in every 32-cell word (decode worst case)
+    "comb70x20": lambda: maps.to_rows(np.array([[(x % 2 == 0) or (y % 3 == 0) for x in range(70)]
+                                                 for y in range(20)])),
 }
 
 
@@ -55,6 +58,7 @@ def _check(rows, goals, **env):
 
 
 def _goals(rows, n, seed):
+    """Up to n distinct free cells (seeded)."""
     cells = maps.rows_to_array(rows)
     free = np.flatnonzero(cells.reshape(-1) != ord("@"))
     rng = np.random.default_rng(seed)
