@@ -1,0 +1,425 @@
+// tsw_bfs_blk.hip — K1 v3: k_bfs_blk, batched per-goal BFS distance tables over 8x8 CELL
+// BLOCKS, one wavefront per goal.
+//
+// What it computes: for goal g, dist[c] = BFS distance from g to every cell c of the
+// 4-connected grid (tswap.rs:44-77 graph), 0xFFFF for blocked/unreachable cells — the same
+// table k_bfs / k_bfs_wave write; get_path's path length - 1 (tswap.rs:288-390).
+//
+// Why blocks: k_bfs_wave works on 32x1 row words. A BFS frontier is a Manhattan ring, i.e.
+// diagonal, so a row word gains about one cell per level and stays on the active list for
+// ~32 levels; on den520d that is ~18 activations per word. An 8x8 block (one u64 per
+// bitmap) is crossed by a diagonal front in ~16 levels and holds 64 cells, so activations
+// per cell drop ~4x while the per-activation bit logic stays a handful of 64-bit ops.
+//
+// Layout (gfx950, 64-lane waves, 160 KiB LDS):
+//  * block (bx, by) of the W x H grid sits at p = (by + 1) * Bp + bx, Bp = BW + 1: a zero
+//    guard block ends every block row and a zero guard row lies above and below, so the
+//    four neighbour blocks are p-1, p+1, p-Bp, p+Bp. Bit (r*8 + c) of a block word is cell
+//    (8bx + c, 8by + r). Block origins are even, so the grid's checkerboard parity is a
+//    fixed mask (CB_EVEN) inside every block.
+//  * LDS: the free-cell blocks FR (shared by the workgroup's waves); per wave the visited
+//    blocks V, two interleaved dedup flag bitmaps and two active-block lists. Goals in
+//    flight per CU are bounded by LDS and the level loop is latency-bound, so the west-step
+//    blocks WL (bit set = the west neighbour was reached one level earlier; written once per
+//    activation, read only by the decode) live in per-wave global scratch, updated with
+//    fire-and-forget 64-bit atomic ORs.
+//  * Level lvl processes exactly the blocks that gain cells at distance lvl:
+//    new = expand(V & parity(lvl-1)) & FR & ~V (race-free inside the wave: the 4-grid is
+//    bipartite, so bits written during a level are never sources in the same level).
+//    Pushes are exact (a neighbour block is queued only if one of its free unvisited cells
+//    touches a new cell), deduplicated with an LDS test-and-set, appended with ballot+mbcnt.
+//  * Distances are not stored per cell during the BFS: along a row run d(x) = d(x-1) +- 1,
+//    recorded by WL, plus one anchor (u16 level, per-wave global scratch) per run start —
+//    a free cell whose west is blocked or whose x is a multiple of 32.
+//  * Decode: one lane per 32-cell row word gathers its 4 blocks' row bytes and rebuilds the
+//    u16 distances (run index table in LDS, bank-conflict-free), 16-B stores, row-major.
+// Algorithmic bytes per goal: 2*W*H table write + ceil(W*H/8) bitmap read.
+#include <hip/hip_runtime.h>
+
+#include "tsw_internal.h"
+#include "tsw_launch.h"
+
+namespace tsw {
+
+namespace {
+
+constexpr uint64_t COL0 = 0x0101010101010101ull;
+constexpr uint64_t COL7 = 0x8080808080808080ull;
+constexpr uint64_t CB_EVEN = 0xAA55AA55AA55AA55ull;  // cells with (r + c) even (row 0 = low byte)
+constexpr uint32_t CT_U16 = 1152;                     // decode run table: 18 rows x 64 lanes u16
+
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void full_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t ld_nc16(const uint16_t* p) { return __builtin_nontemporal_load(p); }
+
+__device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
+
+__device__ __attribute__((noinline)) void blk_list_put_slow(uint16_t* Ln, uint16_t* On, uint32_t cap, uint32_t pos,
+                                                           uint32_t entry) {
+  if (pos < cap) Ln[pos] = (uint16_t)entry;
+  else __builtin_nontemporal_store((uint16_t)entry, On + (pos - cap));
+}
+
+// u16 slot of run-table row j for this lane: lane l's entries live in bank (l & 31), two rows
+// per dword, so the 32 lanes of a group never share a bank whatever rows they read.
+__device__ __forceinline__ uint32_t ct_slot(uint32_t lane, uint32_t j) {
+  return 2u * ((lane & 31u) + 32u * ((j >> 1) + 9u * (lane >> 5))) + (j & 1u);
+}
+
+}  // namespace
+
+// LDS dwords of one wave; must match the carve in k_bfs_blk.
+__host__ __device__ __forceinline__ uint32_t blk_bfs_words(uint32_t nbp, uint32_t nfk, uint32_t cap) {
+  const uint32_t ls = 2u * cap < CT_U16 ? CT_U16 : 2u * cap;  // u16 entries: two lists or the run table
+  return 2u * nbp + 2u * nfk + ((ls + 1u) >> 1);
+}
+
+__global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
+  extern __shared__ __align__(16) uint64_t smem64[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
+  const uint32_t W = A.W, Bp = A.Bp, nbp = A.nbp, cap = A.cap, BW = A.BW;
+  const uint32_t nfk = 1u << A.klog, kmask = nfk - 1u, klog = A.klog;
+  uint64_t* FRs = smem64;
+  uint64_t* V;
+  uint32_t* FL;  // 2 * nfk interleaved flag dwords: block t -> dword t & kmask, bit t >> klog
+  uint16_t* LS;  // 2 * cap list entries / decode run table
+  {
+    uint32_t* b = reinterpret_cast<uint32_t*>(smem64 + nbp) + wv * blk_bfs_words(nbp, nfk, cap);
+    V = reinterpret_cast<uint64_t*>(b);
+    FL = b + 2u * nbp;
+    LS = reinterpret_cast<uint16_t*>(FL + 2u * nfk);
+  }
+  for (uint32_t t = tid; t < nbp; t += blockDim.x) FRs[t] = A.frb[t];
+  __syncthreads();  // the only workgroup barrier: waves run their goals independently
+
+  const uint32_t gw = blockIdx.x * nwv + wv;
+  uint16_t* anch = A.anch + (uint64_t)gw * nbp * 64u;  // anchor of cell bit b of block p at p*64+b
+  uint16_t* lovf = A.lovf + (uint64_t)gw * 2u * nbp;
+  unsigned long long* WL = A.wlg + (uint64_t)gw * nbp;
+  const uint32_t idle_p = Bp + BW;  // guard block of block row 0: FR = 0, all neighbours in range
+  uint64_t t_bfs = 0, t_dec = 0, n_lvl = 0, n_chunk = 0;
+
+  for (;;) {
+    uint32_t gi = 0;
+    if (lane == 0) gi = atomicAdd(A.work, 1u);
+    gi = __builtin_amdgcn_readfirstlane(gi);
+    if (gi >= A.k) break;
+    const uint64_t t0 = clk();
+    const uint32_t goal = A.goals[gi];
+    const uint64_t slot = A.slots ? A.slots[gi] : gi;
+    const uint32_t gy = goal / W, gx = goal - gy * W;
+    const uint32_t gpar = (gx + gy) & 1u;
+
+    for (uint32_t t = lane; t < nbp; t += 64u) {
+      V[t] = 0ull;
+      WL[t] = 0ull;
+    }
+    for (uint32_t t = lane; t < 2u * nfk; t += 64u) FL[t] = 0u;
+    // the WL zeroing stores complete before this goal's atomics are issued
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+
+    uint32_t nn = 0;
+    bool bad = false;
+    // exact pushes of block p whose new cells (distance lvl) are nw: queue the blocks that gain
+    // a cell at lvl + 1 into list Ln (flags Fn). Wave-uniform call; inactive lanes pass nw = 0.
+    auto push = [&](uint32_t p, uint64_t nw, uint64_t vv, uint64_t f0, uint64_t fw, uint64_t fe, uint64_t fn,
+                    uint64_t fs, uint64_t vw, uint64_t ve, uint64_t vn, uint64_t vs, uint32_t* Fn, uint16_t* Ln,
+                    uint16_t* On) {
+      const uint64_t in = ((nw << 1) & ~COL0) | ((nw >> 1) & ~COL7) | (nw << 8) | (nw >> 8);
+      bool w_self = (in & f0 & ~vv) != 0ull;
+      bool w_w = (((nw & COL0) << 7) & fw & ~vw) != 0ull;
+      bool w_e = (((nw & COL7) >> 7) & fe & ~ve) != 0ull;
+      bool w_n = ((nw << 56) & fn & ~vn) != 0ull;
+      bool w_s = ((nw >> 56) & fs & ~vs) != 0ull;
+      const uint32_t tw = p - 1u, te = p + 1u, tn = p - Bp, ts = p + Bp;
+      // dedup: test-and-set on the next level's interleaved flags. All five atomics issue back
+      // to back and are waited for once; a lane that does not want a target ORs 0 into its own
+      // dword (a no-op that conflicts with nobody).
+      auto tas = [&](bool w, uint32_t t) -> uint32_t {
+        const uint32_t m = w ? 1u << (t >> klog) : 0u;
+        return atomicOr(&Fn[w ? (t & kmask) : lane], m) & m;
+      };
+      const uint32_t o_self = tas(w_self, p), o_w = tas(w_w, tw), o_e = tas(w_e, te), o_n = tas(w_n, tn),
+                     o_s = tas(w_s, ts);
+      w_self = w_self && !o_self;
+      w_w = w_w && !o_w;
+      w_e = w_e && !o_e;
+      w_n = w_n && !o_n;
+      w_s = w_s && !o_s;
+      const bool lds_only = nn + 5u * 64u <= cap;
+      auto append = [&](bool c, uint32_t entry) {
+        const uint64_t m = __ballot(c);
+        if (c) {
+          const uint32_t pos = nn + lane_rank(m);
+          if (lds_only) Ln[pos] = (uint16_t)entry;
+          else blk_list_put_slow(Ln, On, cap, pos, entry);
+        }
+        nn += (uint32_t)__popcll(m);
+      };
+      append(w_self, p);
+      append(w_w, tw);
+      append(w_e, te);
+      append(w_n, tn);
+      append(w_s, ts);
+    };
+    // run starts of block p among cells nw: free cells whose west is blocked, or with x % 32 == 0
+    auto anchors = [&](uint32_t p, uint64_t nw, uint64_t f0, uint64_t fw, uint32_t lvl) {
+      const uint32_t bx = p - __umulhi(p, A.bp_magic) * Bp;
+      const uint64_t wf = ((f0 << 1) & ~COL0) | ((bx & 3u) ? ((fw >> 7) & COL0) : 0ull);
+      uint64_t rsn = nw & ~wf;
+      while (rsn) {
+        const uint32_t bb = (uint32_t)__builtin_ctzll(rsn);
+        anch[p * 64u + bb] = (uint16_t)lvl;
+        rsn &= rsn - 1ull;
+      }
+    };
+
+    // ---- level 0: the goal cell; queue the blocks that gain cells at distance 1 ----------
+    uint32_t ncur = 0;
+    {
+      const uint32_t gp = ((gy >> 3) + 1u) * Bp + (gx >> 3);
+      const uint64_t gm = 1ull << (((gy & 7u) << 3) | (gx & 7u));
+      const bool act = lane == 0u;
+      const uint32_t p = act ? gp : idle_p;
+      const uint64_t nw = act ? gm : 0ull;
+      const uint64_t f0 = FRs[p], fw = FRs[p - 1u], fe = FRs[p + 1u], fn = FRs[p - Bp], fs = FRs[p + Bp];
+      if (act) {
+        V[p] = gm;
+        anchors(p, nw, f0, fw, 0u);
+      }
+      push(p, nw, nw, f0, fw, fe, fn, fs, 0ull, 0ull, 0ull, 0ull, FL, LS, lovf);
+      ncur = nn;
+      lds_sync();
+    }
+
+    // ---- levels 1, 2, ...: process the blocks that gain cells at distance lvl -------------
+    uint32_t cur = 0;
+    uint32_t lvl = 1;
+    while (ncur != 0u) {
+      if (lvl >= 0xFFFFu) {
+        if (lane == 0) atomicOr(A.err, ERR_DIST_OVERFLOW);
+        break;
+      }
+      const uint32_t nxt = cur ^ 1u;
+      const uint16_t* Lc = LS + cur * cap;
+      uint16_t* Ln = LS + nxt * cap;
+      const uint16_t* Oc = lovf + cur * nbp;
+      uint16_t* On = lovf + nxt * nbp;
+      uint32_t* Fc = FL + cur * nfk;
+      uint32_t* Fn = FL + nxt * nfk;
+      const uint64_t pnew = ((gpar + lvl) & 1u) ? ~CB_EVEN : CB_EVEN;  // cells at distance lvl
+      const uint64_t psrc = ~pnew;                                      // cells at distance lvl-1
+      nn = 0;
+      // one chunk: lane's list entry p (idle lanes: the guard block idle_p, act = false)
+      auto chunk = [&](uint32_t p, bool act) {
+        const uint64_t v0 = V[p], vw = V[p - 1u], ve = V[p + 1u], vn = V[p - Bp], vs = V[p + Bp];
+        const uint64_t f0 = FRs[p], fw = FRs[p - 1u], fe = FRs[p + 1u], fn = FRs[p - Bp], fs = FRs[p + Bp];
+        const uint64_t a = v0 & psrc, aw = vw & psrc, ae = ve & psrc, an = vn & psrc, as = vs & psrc;
+        const uint64_t ex = ((a << 1) & ~COL0) | ((a >> 1) & ~COL7) | ((aw >> 7) & COL0) | ((ae << 7) & COL7) |
+                            (a << 8) | (a >> 8) | (an >> 56) | (as << 56);
+        const uint64_t nw = ex & f0 & ~v0;  // 0 for idle lanes (FR of the guard block is 0)
+        const uint64_t vv = v0 | nw;
+        // owner-exclusive within the level (the list is deduplicated); idle lanes rewrite the
+        // zero guard block
+        V[p] = vv;
+        const uint64_t wln = nw & (((v0 << 1) & ~COL0) | ((vw >> 7) & COL0));
+        if (wln) atomicOr(WL + p, (unsigned long long)wln);
+        bad |= act && nw == 0ull;  // entries must gain a cell
+        anchors(p, nw, f0, fw, lvl);
+        push(p, nw, vv, f0, fw, fe, fn, fs, vw, ve, vn, vs, Fn, Ln, On);
+        ++n_chunk;
+      };
+      if (ncur <= cap) {
+        // LDS-only list (wave-uniform): no global load in the loop, so nothing waits for the
+        // wave's outstanding anchor stores; entries prefetched one chunk ahead
+        uint32_t e_next = lane < ncur ? (uint32_t)Lc[lane] : idle_p;
+        for (uint32_t b0 = 0; b0 < ncur; b0 += 64u) {
+          const uint32_t p = e_next;
+          const uint32_t i = b0 + 64u + lane;
+          e_next = i < ncur ? (uint32_t)Lc[i] : idle_p;
+          chunk(p, b0 + lane < ncur);
+        }
+      } else {
+        for (uint32_t b0 = 0; b0 < ncur; b0 += 64u) {
+          const uint32_t i = b0 + lane;
+          const uint32_t p = i >= ncur ? idle_p : i < cap ? (uint32_t)Lc[i] : ld_nc16(Oc + (i - cap));
+          chunk(p, i < ncur);
+        }
+      }
+      // the flags of this level's list are reused two levels later
+      for (uint32_t t = lane; t < nfk; t += 64u) Fc[t] = 0u;
+      if (nn > cap) full_sync();  // overflow entries went to global memory
+      else lds_sync();
+      cur = nxt;
+      ncur = nn;
+      ++lvl;
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(A.err, ERR_BFS_LIST);
+    full_sync();  // anchors (global) complete before the decode reads them
+    const uint64_t t1 = clk();
+
+    // ---- decode + write-out: one 32-cell row word per lane per iteration ------------------
+    // d(b) = F(b) + C(run(b)): F(b) = 2*popc(WL & bits<=b) - (b+1) is the +-1 walk from bit 0,
+    // C(j) = A(j) - F(s_j) for run j starting at bit s_j with anchor A(j) (mod 2^16: the table
+    // is u16). Bit b belongs to run popc(rsw & bits<=b) - 1 (<= 16 runs per word); C goes to row
+    // popc(...) of this lane's column of the run table.
+    const uint8_t* V8 = reinterpret_cast<const uint8_t*>(V);
+    const uint8_t* WL8 = reinterpret_cast<const uint8_t*>(WL);  // global, L2-resident
+    const uint8_t* FR8 = reinterpret_cast<const uint8_t*>(FRs);
+    uint16_t* D = A.dist + slot * A.dstride;
+    const uint32_t Ww = (W + 31u) >> 5, nwords = A.H * Ww;
+    const float invWw = 1.0f / (float)Ww;
+    // row word k -> (y, cw), its first block p0 and row-in-block r; bitmaps gathered from the 4
+    // blocks' row bytes; the first 4 run anchors are loaded one iteration ahead (L2 latency)
+    struct Word {
+      uint32_t y, cw, r, p0, vis, wl, f0, a[4];
+    };
+    auto fetch = [&](uint32_t k, Word& o) {
+      uint32_t y = (uint32_t)((float)k * invWw);
+      while (y * Ww > k) --y;
+      while ((y + 1u) * Ww <= k) ++y;
+      o.y = y;
+      o.cw = k - y * Ww;
+      o.r = y & 7u;
+      o.p0 = ((y >> 3) + 1u) * Bp + 4u * o.cw;
+      o.vis = o.wl = o.f0 = 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        if (4u * o.cw + j < BW) {
+          const uint32_t off = (o.p0 + j) * 8u + o.r;
+          o.vis |= (uint32_t)V8[off] << (8u * j);
+          o.wl |= (uint32_t)__builtin_nontemporal_load(WL8 + off) << (8u * j);
+          o.f0 |= (uint32_t)FR8[off] << (8u * j);
+        }
+      }
+      // unconditional loads (a run-less slot reads the word's first cell, unused), so the
+      // compiler can count them in vmcnt instead of draining at a branch merge
+      uint32_t rs = o.f0 & ~(o.f0 << 1);
+#pragma unroll
+      for (uint32_t j = 0; j < 4u; ++j) {
+        const uint32_t sj = rs ? (uint32_t)__builtin_ctz(rs) : 0u;
+        o.a[j] = ld_nc16(anch + (o.p0 + (sj >> 3)) * 64u + o.r * 8u + (sj & 7u));
+        rs &= rs - 1u;
+      }
+    };
+    // two words in flight: the decode of one overlaps the other's anchor loads
+    auto decode = [&](const Word& cu) {
+      const uint32_t y = cu.y, cw = cu.cw, r = cu.r, p0 = cu.p0, vis = cu.vis, wl = cu.wl, f0 = cu.f0;
+      const uint32_t rsw = f0 & ~(f0 << 1);
+      uint32_t pk[16];
+      if (vis != 0u) {
+        // runs 1..4: branch-free with the prefetched anchors (rows past the last run are never
+        // looked up); runs 5..16 (rare) load their anchors here
+        uint32_t rs = rsw;
+#pragma unroll
+        for (uint32_t j = 1; j <= 4u; ++j) {
+          const uint32_t sj = rs ? (uint32_t)__builtin_ctz(rs) : 0u;
+          rs &= rs - 1u;
+          const uint32_t Fs = 2u * __popc(wl & (0xFFFFFFFFu >> (31u - sj))) - (sj + 1u);
+          LS[ct_slot(lane, j)] = (uint16_t)(cu.a[j - 1u] - Fs);  // own column: program order suffices
+        }
+        for (uint32_t j = 5; rs != 0u; ++j) {
+          const uint32_t sj = __builtin_ctz(rs);
+          rs &= rs - 1u;
+          const uint32_t Aj = ld_nc16(anch + (p0 + (sj >> 3)) * 64u + r * 8u + (sj & 7u));
+          const uint32_t Fs = 2u * __popc(wl & (0xFFFFFFFFu >> (31u - sj))) - (sj + 1u);
+          LS[ct_slot(lane, j)] = (uint16_t)(Aj - Fs);
+        }
+#pragma unroll
+        for (int b = 0; b < 32; ++b) {
+          const uint32_t m = 0xFFFFFFFFu >> (31 - b);
+          const uint32_t C = LS[ct_slot(lane, (uint32_t)__popc(rsw & m))];
+          const uint32_t F = 2u * __popc(wl & m) - (uint32_t)(b + 1);
+          const uint32_t v = ((vis >> b) & 1u) ? ((F + C) & 0xFFFFu) : 0xFFFFu;
+          if (b & 1) pk[b >> 1] |= v << 16;
+          else pk[b >> 1] = v;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pk[j] = 0xFFFFFFFFu;
+      }
+      const uint32_t x0 = cw << 5;
+      const uint32_t cnt = min(32u, W - x0);
+      uint16_t* dst = D + (uint64_t)y * W + x0;
+      if (A.vec16 && cnt == 32u) {
+        uint4* q = reinterpret_cast<uint4*>(dst);
+        q[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        q[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+        q[2] = make_uint4(pk[8], pk[9], pk[10], pk[11]);
+        q[3] = make_uint4(pk[12], pk[13], pk[14], pk[15]);
+      } else {
+#pragma unroll
+        for (uint32_t b = 0; b < 32u; ++b)
+          if (b < cnt) dst[b] = (uint16_t)(pk[b >> 1] >> ((b & 1u) * 16u));
+      }
+    };
+    Word wa{}, wb{};
+    if (lane < nwords) fetch(lane, wa);
+    for (uint32_t k = lane; k < nwords; k += 128u) {
+      if (k + 64u < nwords) fetch(k + 64u, wb);
+      decode(wa);
+      if (k + 128u < nwords) fetch(k + 128u, wa);
+      if (k + 64u < nwords) decode(wb);
+    }
+    lds_sync();  // the next goal re-initialises this wave's LDS
+    if (A.prof) {
+      const uint64_t t2 = clk();
+      t_bfs += t1 - t0;
+      t_dec += t2 - t1;
+      n_lvl += lvl;
+    }
+  }
+  if (A.prof && lane == 0) {
+    atomicAdd((unsigned long long*)&A.prof[0], (unsigned long long)t_bfs);
+    atomicAdd((unsigned long long*)&A.prof[1], (unsigned long long)t_dec);
+    atomicAdd((unsigned long long*)&A.prof[2], (unsigned long long)n_lvl);
+    atomicAdd((unsigned long long*)&A.prof[3], (unsigned long long)n_chunk);
+  }
+}
+
+uint32_t bfs_blk_klog(uint32_t nbp) {
+  uint32_t kl = 6;
+  while ((32u << kl) < nbp) ++kl;
+  return kl;
+}
+
+uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds) {
+  const size_t per_wave = (size_t)blk_bfs_words(nbp, 1u << bfs_blk_klog(nbp), cap) * 4u;
+  const size_t shared = (size_t)nbp * 8u;
+  if (max_lds <= 0 || shared + per_wave > (size_t)max_lds) return 0;
+  return (uint32_t)std::min<size_t>(16u, ((size_t)max_lds - shared) / per_wave);
+}
+
+hipError_t launch_bfs_blk(const BlkBfsArgs& A0, int max_lds, int num_cu, hipStream_t s) {
+  if (A0.k == 0) return hipSuccess;
+  BlkBfsArgs A = A0;
+  A.klog = bfs_blk_klog(A.nbp);
+  A.bp_magic = (uint32_t)((0xFFFFFFFFull + A.Bp) / A.Bp);  // ceil(2^32 / Bp): exact p / Bp for p*Bp < 2^32
+  const size_t per_wave = (size_t)blk_bfs_words(A.nbp, 1u << A.klog, A.cap) * 4u;
+  const size_t shared = (size_t)A.nbp * 8u;
+  const uint32_t nwv = std::min<uint32_t>(A.max_waves, bfs_blk_waves_per_block(A.nbp, A.cap, max_lds));
+  if (nwv == 0 || A.nbp > 0x10000u || A.cap > 0x8000u) return hipErrorInvalidValue;
+  const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cu, (A.k + nwv - 1u) / nwv));
+  if ((uint64_t)grid * nwv > A.scratch_waves) return hipErrorInvalidValue;
+  const size_t lds = shared + nwv * per_wave;
+  hipError_t e = hipFuncSetAttribute((const void*)k_bfs_blk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_bfs_blk, dim3(grid), dim3(nwv * 64u), lds, s, A);
+  return hipGetLastError();
+}
+
+}  // namespace tsw

@@ -53,11 +53,17 @@ struct tsw_ctx {
   uint32_t* d_freebits = nullptr;
   int max_lds = 65536, num_cu = 256;
   // K1 v2 (k_bfs_wave) padded grid + per-wave scratch
-  uint32_t Wp = 0, npw = 0, bfs_cap = 512, bfs_mode = 0;  // mode 0 auto, 1 wave, 2 block
+  uint32_t Wp = 0, npw = 0, bfs_cap = 512, bfs_mode = 0;  // mode 0 auto, 1 wave, 2 block, 3 blk8
   uint32_t* d_frp = nullptr;
+  // K1 v3 (k_bfs_blk) 8x8-block grid
+  uint32_t BW = 0, BH = 0, Bp = 0, nbp = 0, blk_cap = 576;
+  uint64_t* d_frb = nullptr;
+  unsigned long long* d_wlg = nullptr;  // k_bfs_blk per-wave WL scratch
+  uint64_t wlg_waves = 0;
   uint16_t* d_anch = nullptr;
   uint16_t* d_lovf = nullptr;
   uint64_t wave_scratch = 0;
+  size_t scratch_words = 0, scratch_lwords = 0;
   unsigned long long* d_bprof = nullptr;  // TSW_BFS_PROF=1: k_bfs_wave cycle split, printed per launch
 
   // goal-table store
@@ -375,11 +381,97 @@ bool eager_policy(const tsw_ctx* c, size_t new_tables) {
 // K1 over k goals (device arrays; slots may be null = goal index): the wave-per-goal kernel
 // when its LDS fits, else the workgroup-per-goal kernel. Next-hop codes (nh != null) come
 // fused from k_bfs, or from k_classify over the finished tables after k_bfs_wave.
+// per-wave scratch of the wave-per-goal kernels: `words` u16 anchors + `lwords` u16 list overflow
+int ensure_wave_scratch(tsw_ctx* c, uint64_t want, size_t words, size_t lwords) {
+  if (want <= c->wave_scratch && words <= c->scratch_words && lwords <= c->scratch_lwords) return TSW_OK;
+  want = std::max(want, c->wave_scratch);
+  words = std::max(words, c->scratch_words);
+  lwords = std::max(lwords, c->scratch_lwords);
+  HIPCHK(hipStreamSynchronize(c->s));
+  if (c->d_anch) HIPCHK(hipFree(c->d_anch));
+  if (c->d_lovf) HIPCHK(hipFree(c->d_lovf));
+  c->d_anch = nullptr;
+  c->d_lovf = nullptr;
+  c->wave_scratch = 0;
+  HIPCHK(hipMalloc(&c->d_anch, (size_t)want * words * 2u));
+  HIPCHK(hipMalloc(&c->d_lovf, (size_t)want * lwords * 2u));
+  c->wave_scratch = want;
+  c->scratch_words = words;
+  c->scratch_lwords = lwords;
+  return TSW_OK;
+}
+
+unsigned long long* bfs_prof_buf(tsw_ctx* c) {
+  if (!getenv("TSW_BFS_PROF")) return nullptr;
+  if (!c->d_bprof && hipMalloc(&c->d_bprof, 4 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(c->d_bprof, 0, 4 * sizeof(unsigned long long), c->s) != hipSuccess) return nullptr;
+  return c->d_bprof;
+}
+
+int bfs_prof_print(tsw_ctx* c, const char* name, uint32_t k) {
+  unsigned long long h[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(h, c->d_bprof, sizeof h, hipMemcpyDeviceToHost, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  fprintf(stderr, "[%s] goals %u  bfs %.0f cyc/goal  decode %.0f cyc/goal  levels %.1f/goal  chunks %.1f/goal\n",
+          name, k, (double)h[0] / k, (double)h[1] / k, (double)h[2] / k, (double)h[3] / k);
+  return TSW_OK;
+}
+
+// K1 over k goals (device arrays; slots may be null = goal index): the 8x8-block wave-per-goal
+// kernel when its LDS fits, else the row-word wave-per-goal kernel, else the workgroup-per-goal
+// kernel. Next-hop codes (nh != null) come fused from k_bfs, or from k_classify over the
+// finished tables after the wave kernels.
 int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k, uint16_t* dist, uint64_t dstride,
             uint8_t* nh) {
   if (k == 0) return TSW_OK;
+  const bool vec16 = c->G.W % 8u == 0u && dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u;
+  const uint32_t max_waves = getenv("TSW_BFS_WAVES") ? (uint32_t)std::max(1, atoi(getenv("TSW_BFS_WAVES"))) : 16u;
+  uint32_t nbw = 0;
+  if ((c->bfs_mode == 0 || c->bfs_mode == 3) && c->nbp <= 0x10000u)
+    nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->blk_cap, c->max_lds));
+  if (nbw == 0 && c->bfs_mode == 3) RET(TSW_EINVAL, "k_bfs_blk does not fit this grid (TSW_BFS_KERNEL=blk)");
+  if (nbw > 0) {
+    Timer t(c, CAT_BFS);
+    TRY(ensure_wave_scratch(c, (uint64_t)c->num_cu * nbw, (size_t)c->nbp * 64u, (size_t)c->nbp * 2u));
+    if (c->wlg_waves < c->wave_scratch) {
+      HIPCHK(hipStreamSynchronize(c->s));
+      if (c->d_wlg) HIPCHK(hipFree(c->d_wlg));
+      c->d_wlg = nullptr;
+      c->wlg_waves = 0;
+      HIPCHK(hipMalloc(&c->d_wlg, (size_t)c->wave_scratch * c->nbp * 8u));
+      c->wlg_waves = c->wave_scratch;
+    }
+    BlkBfsArgs A{};
+    A.W = c->G.W;
+    A.H = c->G.H;
+    A.BW = c->BW;
+    A.BH = c->BH;
+    A.Bp = c->Bp;
+    A.nbp = c->nbp;
+    A.cap = c->blk_cap;
+    A.frb = c->d_frb;
+    A.goals = goals;
+    A.slots = slots;
+    A.k = k;
+    A.dist = dist;
+    A.dstride = dstride;
+    A.anch = c->d_anch;
+    A.lovf = c->d_lovf;
+    A.wlg = c->d_wlg;
+    A.work = &c->d_stat->work;
+    A.err = &c->d_stat->err;
+    A.vec16 = vec16 ? 1u : 0u;
+    A.max_waves = nbw;
+    A.scratch_waves = std::min(c->wave_scratch, c->wlg_waves);
+    A.prof = (uint64_t*)bfs_prof_buf(c);
+    HIPCHK(hipMemsetAsync(&c->d_stat->work, 0, 4, c->s));
+    HIPCHK(launch_bfs_blk(A, c->max_lds, c->num_cu, c->s));
+    if (A.prof) TRY(bfs_prof_print(c, "k_bfs_blk", k));
+    if (nh) HIPCHK(launch_classify(c->G, goals, slots, k, dist, dstride, nh, c->s));
+    return TSW_OK;
+  }
   uint32_t nwv = 0;
-  if (c->bfs_mode != 2 && c->npw <= 0x8000u)
+  if ((c->bfs_mode == 0 || c->bfs_mode == 1) && c->npw <= 0x8000u)
     nwv = bfs_wave_waves_per_block(c->npw, c->bfs_cap, c->max_lds);
   if (nwv == 0 && c->bfs_mode == 1) RET(TSW_EINVAL, "k_bfs_wave does not fit this grid (TSW_BFS_KERNEL=wave)");
   Timer t(c, CAT_BFS);
@@ -388,18 +480,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
                       c->s));
     return TSW_OK;
   }
-  const uint64_t want = (uint64_t)c->num_cu * nwv;
-  if (want > c->wave_scratch) {
-    HIPCHK(hipStreamSynchronize(c->s));
-    if (c->d_anch) HIPCHK(hipFree(c->d_anch));
-    if (c->d_lovf) HIPCHK(hipFree(c->d_lovf));
-    c->d_anch = nullptr;
-    c->d_lovf = nullptr;
-    c->wave_scratch = 0;
-    HIPCHK(hipMalloc(&c->d_anch, (size_t)want * c->npw * 32u * 2u));
-    HIPCHK(hipMalloc(&c->d_lovf, (size_t)want * 2u * c->npw * 2u));
-    c->wave_scratch = want;
-  }
+  TRY(ensure_wave_scratch(c, (uint64_t)c->num_cu * nwv, (size_t)c->npw * 32u, (size_t)c->npw * 2u));
   WaveBfsArgs A{};
   A.W = c->G.W;
   A.H = c->G.H;
@@ -417,24 +498,13 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   A.lovf = c->d_lovf;
   A.work = &c->d_stat->work;
   A.err = &c->d_stat->err;
-  A.vec16 = (c->G.W % 8u == 0u && dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u) ? 1u : 0u;
-  A.max_waves = getenv("TSW_BFS_WAVES") ? (uint32_t)std::max(1, atoi(getenv("TSW_BFS_WAVES"))) : 16u;
+  A.vec16 = vec16 ? 1u : 0u;
+  A.max_waves = max_waves;
   A.scratch_waves = c->wave_scratch;
-  A.prof = nullptr;
-  if (getenv("TSW_BFS_PROF")) {
-    if (!c->d_bprof) HIPCHK(hipMalloc(&c->d_bprof, 4 * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(c->d_bprof, 0, 4 * sizeof(unsigned long long), c->s));
-    A.prof = (uint64_t*)c->d_bprof;
-  }
+  A.prof = (uint64_t*)bfs_prof_buf(c);
   HIPCHK(hipMemsetAsync(&c->d_stat->work, 0, 4, c->s));
   HIPCHK(launch_bfs_wave(A, c->max_lds, c->num_cu, c->s));
-  if (A.prof) {
-    unsigned long long h[4] = {0, 0, 0, 0};
-    HIPCHK(hipMemcpyAsync(h, c->d_bprof, sizeof h, hipMemcpyDeviceToHost, c->s));
-    HIPCHK(hipStreamSynchronize(c->s));
-    fprintf(stderr, "[k_bfs_wave] goals %u  bfs %.0f cyc/goal  decode %.0f cyc/goal  levels %.1f/goal  chunks %.1f/goal\n",
-            k, (double)h[0] / k, (double)h[1] / k, (double)h[2] / k, (double)h[3] / k);
-  }
+  if (A.prof) TRY(bfs_prof_print(c, "k_bfs_wave", k));
   if (nh) HIPCHK(launch_classify(c->G, goals, slots, k, dist, dstride, nh, c->s));
   return TSW_OK;
 }
@@ -801,8 +871,23 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
     if ((e = hipMalloc(&c->d_frp, (size_t)c->npw * 4)) != hipSuccess) return fail("malloc frp", e);
     if ((e = hipMemcpy(c->d_frp, frp.data(), (size_t)c->npw * 4, hipMemcpyHostToDevice)) != hipSuccess)
       return fail("copy frp", e);
-    if (const char* m = getenv("TSW_BFS_KERNEL")) c->bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : 0u;
+    // k_bfs_blk layout: block (bx, by) at (by + 1) * Bp + bx, zero guard block column and rows
+    c->BW = (w + 7u) / 8u;
+    c->BH = (h + 7u) / 8u;
+    c->Bp = c->BW + 1u;
+    c->nbp = (c->BH + 2u) * c->Bp;
+    std::vector<uint64_t> frb(c->nbp, 0ull);
+    for (uint32_t y = 0; y < h; ++y)
+      for (uint32_t x = 0; x < w; ++x)
+        if (c->h_nbmask[(size_t)y * w + x] & NB_FREE)
+          frb[(size_t)((y >> 3) + 1u) * c->Bp + (x >> 3)] |= 1ull << (((y & 7u) << 3) | (x & 7u));
+    if ((e = hipMalloc(&c->d_frb, (size_t)c->nbp * 8)) != hipSuccess) return fail("malloc frb", e);
+    if ((e = hipMemcpy(c->d_frb, frb.data(), (size_t)c->nbp * 8, hipMemcpyHostToDevice)) != hipSuccess)
+      return fail("copy frb", e);
+    if (const char* m = getenv("TSW_BFS_KERNEL"))
+      c->bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : !strcmp(m, "blk") ? 3u : 0u;
     if (const char* m = getenv("TSW_BFS_LISTCAP")) c->bfs_cap = std::max(1, std::min(atoi(m), 32768));
+    if (const char* m = getenv("TSW_BFS_BLKCAP")) c->blk_cap = std::max(1, std::min(atoi(m), 32768));
   }
   c->h_goal_tab.assign(ncell, -1);
   if ((e = hipMalloc(&c->d_goal_tab, (size_t)ncell * 4)) != hipSuccess) return fail("malloc goal_tab", e);
@@ -835,7 +920,7 @@ void tsw_destroy(tsw_ctx* c) {
   auto fre = [](void* p) {
     if (p) (void)hipFree(p);
   };
-  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_anch); fre(c->d_lovf); fre(c->d_bprof); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
+  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_frb); fre(c->d_wlg); fre(c->d_anch); fre(c->d_lovf); fre(c->d_bprof); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
   fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);

@@ -38,6 +38,29 @@ struct WaveBfsArgs {
 uint32_t bfs_wave_waves_per_block(uint32_t npw, uint32_t cap, int max_lds);
 hipError_t launch_bfs_wave(const WaveBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
 
+// K1 v3 (tsw_bfs_blk.hip): one wavefront per goal over 8x8 cell blocks. Block (bx, by) sits at
+// p = (by + 1) * Bp + bx, Bp = BW + 1 (zero guard block per block row, zero guard block rows).
+struct BlkBfsArgs {
+  uint32_t W, H, BW, BH, Bp, nbp, cap, klog, bp_magic;
+  const uint64_t* frb;    // [nbp] padded free-cell blocks (bit r*8+c = cell (8bx+c, 8by+r))
+  const uint32_t* goals;
+  const uint32_t* slots;  // table slot per goal (nullptr: slot = goal index)
+  uint32_t k;
+  uint16_t* dist;
+  uint64_t dstride;
+  uint16_t* anch;         // per-wave anchor scratch, nbp * 64 u16 each
+  uint16_t* lovf;         // per-wave list overflow, 2 * nbp u16 each
+  unsigned long long* wlg;  // per-wave west-step blocks, nbp u64 each
+  uint32_t* work;         // goal dequeue counter (zeroed before the launch)
+  uint32_t* err;
+  uint32_t vec16;         // 16-B stores allowed (W % 8 == 0, 16-B aligned tables)
+  uint32_t max_waves;
+  uint64_t scratch_waves;
+  uint64_t* prof;         // optional: [bfs cycles, decode cycles, levels, chunks] summed over waves
+};
+uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds);
+hipError_t launch_bfs_blk(const BlkBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
+
 hipError_t launch_classify(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                            const uint16_t* dist_base, uint64_t stride, uint8_t* nh_base, hipStream_t s);
 

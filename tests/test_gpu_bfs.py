@@ -1,5 +1,5 @@
-"""K1 parity: both BFS kernels (k_bfs_wave: one wavefront per goal; k_bfs: one workgroup per
-goal) against the oracle's BFS (oracle/tswap_oracle.c, cross-checked against A* path lengths in
+"""K1 parity: the three BFS kernels (k_bfs_blk: one wavefront per goal over 8x8 blocks;
+k_bfs_wave: one wavefront per goal over row words; k_bfs: one workgroup per goal) against the oracle's BFS (oracle/tswap_oracle.c, cross-checked against A* path lengths in
 test_oracle.py), bit-exact, on ragged widths, list-overflow paths and the full-size den520d-like
 cave (BASELINE configs[3])."""
 import os
@@ -65,7 +65,7 @@ def _goals(rows, n, seed):
     return rng.choice(free, size=min(n, free.size), replace=False).astype(np.uint32)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "block"])
+@pytest.mark.parametrize("kernel", ["blk", "wave", "block"])
 @pytest.mark.parametrize("name", sorted(GRIDS))
 def test_bfs_kernels_bit_exact(kernel, name):
     rows = GRIDS[name]()
@@ -79,7 +79,14 @@ def test_bfs_wave_list_overflow(cap):
     _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="wave", TSW_BFS_LISTCAP=cap)
 
 
-def test_bfs_wave_unreachable_pockets():
+@pytest.mark.parametrize("cap", [1, 3, 17])
+def test_bfs_blk_list_overflow(cap):
+    rows = maps.cave_map(128, 97, 9)
+    _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="blk", TSW_BFS_BLKCAP=cap)
+
+
+@pytest.mark.parametrize("kernel", ["blk", "wave"])
+def test_bfs_wave_unreachable_pockets(kernel):
     """Walled-off pockets stay 0xFFFF; goals inside a pocket see only the pocket."""
     a = np.zeros((40, 70), dtype=bool)
     a[10, :] = True          # full wall: two halves
@@ -89,7 +96,7 @@ def test_bfs_wave_unreachable_pockets():
     cells = maps.rows_to_array(rows)
     goals = np.array([0, 69, 11 * 70 + 5, 22 * 70 + 32, 39 * 70 + 69], dtype=np.uint32)
     assert all(cells.reshape(-1)[g] != ord("@") for g in goals)
-    _check(rows, goals, TSW_BFS_KERNEL="wave")
+    _check(rows, goals, TSW_BFS_KERNEL=kernel)
 
 
 class _DevBuf:
@@ -115,7 +122,8 @@ class _DevBuf:
         self.hip.hipFree(self.ptr)
 
 
-def test_bfs_wave_den520d_full_size():
+@pytest.mark.parametrize("kernel", ["blk", "wave"])
+def test_bfs_den520d_full_size(kernel):
     """BASELINE configs[3] geometry: 256x257 cave, 1,000 distinct goals through the device-output
     entry point the bench times (16-B stores), every table bit-exact vs the oracle."""
     rows = maps.cave_map(256, 257, 0x520D)
@@ -123,7 +131,7 @@ def test_bfs_wave_den520d_full_size():
     og = OracleGraph(cells)
     goals = np.sort(_goals(rows, 1000, 0x520D))
     ncell = 256 * 257
-    with _env(TSW_BFS_KERNEL="wave"), Planner(rows) as p:
+    with _env(TSW_BFS_KERNEL=kernel), Planner(rows) as p:
         buf = _DevBuf(goals.size * ncell * 2)
         p.dist_tables_device(goals, buf.ptr.value)
         got = buf.to_host(np.empty((goals.size, ncell), dtype=np.uint16))
@@ -132,14 +140,15 @@ def test_bfs_wave_den520d_full_size():
         assert np.array_equal(got[k], ref), f"goal {g}: {np.count_nonzero(got[k] != ref)} cells differ"
 
 
-def test_bfs_wave_symmetry_full_goal_set():
+@pytest.mark.parametrize("kernel", ["blk", "wave"])
+def test_bfs_symmetry_full_goal_set(kernel):
     """Size-independent property at full size: d_g(c) == d_c(g) for every pair of goals, over all
     free cells of a 96x97 cave used as goals (the table matrix restricted to goals is symmetric),
     and blocked cells are 0xFFFF in every table."""
     rows = maps.cave_map(96, 97, 0x5EED)
     cells = maps.rows_to_array(rows).reshape(-1)
     free = np.flatnonzero(cells != ord("@")).astype(np.uint32)
-    with _env(TSW_BFS_KERNEL="wave"), Planner(rows) as p:
+    with _env(TSW_BFS_KERNEL=kernel), Planner(rows) as p:
         t = p.dist_tables(free)
     sub = t[:, free].astype(np.int64)
     assert np.array_equal(sub, sub.T)
