@@ -218,6 +218,7 @@ def main():
             del full
         cells_per_s = allsum(float(mine.size * ncell)) * args.bfs_reps / tbw
         k_gbs = mine.size * bytes_goal / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
+        btraffic, btraffic_src = profiled_traffic("k_bfs_blk")
         bfs = {
             "workload": "den520d-like 256x257 cave (seed 0x520D), distinct goals",
             "goals_total": int(goals.size),
@@ -227,6 +228,19 @@ def main():
             "kernel_GBps": round(k_gbs, 2),
             "hbm_frac": round(k_gbs / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_goal": bytes_goal,
+            # K1 against the HBM roofline: algorithmic bytes per launch (u16 table
+            # write + obstacle bitmap read, per goal x goals per launch) / HIP-event launch time
+            "roofline": {
+                "kernel": "k_bfs_blk (K1 batched BFS tables)",
+                "bound": "hbm",
+                "achieved": round(k_gbs, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(k_gbs / HBM_PEAK_GBS, 4),
+                "traffic": btraffic if world == 1 else None,
+                "traffic_source": btraffic_src if world == 1 else None,
+                "algorithmic_bytes_per_launch": int(mine.size * bytes_goal),
+            },
             # N > 1: wall time of (this rank's K1 shard + RCCL all-gather of all tables), max over ranks
             "sharded_build_allgather_ms": round(gather_ms, 3) if gather_ms is not None else None,
         }

@@ -29,8 +29,10 @@
 //    Pushes are exact (a neighbour block is queued only if one of its free unvisited cells
 //    touches a new cell), deduplicated with an LDS test-and-set, appended with ballot+mbcnt.
 //  * Distances are not stored per cell during the BFS: along a row run d(x) = d(x-1) +- 1,
-//    recorded by WL, plus one anchor (u16 level, per-wave global scratch) per run start —
-//    a free cell whose west is blocked or whose x is a multiple of 32.
+//    recorded by WL, plus one anchor (u16 level) per run start — a free cell whose west is
+//    blocked or whose x is a multiple of 32. Anchors are stored COMPACTLY (per-wave global
+//    scratch of nrs u16, run starts numbered in block order: AB[p] + rank inside the block), so
+//    a goal dirties ~2*nrs bytes of cache lines instead of one line per anchor.
 //  * Decode: one lane per 32-cell row word gathers its 4 blocks' row bytes and rebuilds the
 //    u16 distances (run index table in LDS, bank-conflict-free), 16-B stores, row-major.
 // Algorithmic bytes per goal: 2*W*H table write + ceil(W*H/8) bitmap read.
@@ -93,20 +95,24 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   const uint32_t W = A.W, Bp = A.Bp, nbp = A.nbp, cap = A.cap, BW = A.BW;
   const uint32_t nfk = 1u << A.klog, kmask = nfk - 1u, klog = A.klog;
   uint64_t* FRs = smem64;
+  uint32_t* AB = reinterpret_cast<uint32_t*>(smem64 + nbp);  // [nbp] first run-start index of block p
   uint64_t* V;
   uint32_t* FL;  // 2 * nfk interleaved flag dwords: block t -> dword t & kmask, bit t >> klog
   uint16_t* LS;  // 2 * cap list entries / decode run table
   {
-    uint32_t* b = reinterpret_cast<uint32_t*>(smem64 + nbp) + wv * blk_bfs_words(nbp, nfk, cap);
+    uint32_t* b = reinterpret_cast<uint32_t*>(smem64 + nbp + (nbp + 1u) / 2u) + wv * blk_bfs_words(nbp, nfk, cap);
     V = reinterpret_cast<uint64_t*>(b);
     FL = b + 2u * nbp;
     LS = reinterpret_cast<uint16_t*>(FL + 2u * nfk);
   }
-  for (uint32_t t = tid; t < nbp; t += blockDim.x) FRs[t] = A.frb[t];
+  for (uint32_t t = tid; t < nbp; t += blockDim.x) {
+    FRs[t] = A.frb[t];
+    AB[t] = A.abase[t];
+  }
   __syncthreads();  // the only workgroup barrier: waves run their goals independently
 
   const uint32_t gw = blockIdx.x * nwv + wv;
-  uint16_t* anch = A.anch + (uint64_t)gw * nbp * 64u;  // anchor of cell bit b of block p at p*64+b
+  uint16_t* anch = A.anch + (uint64_t)gw * A.nrs;  // compact anchors (run-start index)
   uint16_t* lovf = A.lovf + (uint64_t)gw * 2u * nbp;
   unsigned long long* WL = A.wlg + (uint64_t)gw * nbp;
   const uint32_t idle_p = Bp + BW;  // guard block of block row 0: FR = 0, all neighbours in range
@@ -180,10 +186,11 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
     auto anchors = [&](uint32_t p, uint64_t nw, uint64_t f0, uint64_t fw, uint32_t lvl) {
       const uint32_t bx = p - __umulhi(p, A.bp_magic) * Bp;
       const uint64_t wf = ((f0 << 1) & ~COL0) | ((bx & 3u) ? ((fw >> 7) & COL0) : 0ull);
-      uint64_t rsn = nw & ~wf;
+      const uint64_t rs = f0 & ~wf;
+      uint64_t rsn = nw & rs;
       while (rsn) {
         const uint32_t bb = (uint32_t)__builtin_ctzll(rsn);
-        anch[p * 64u + bb] = (uint16_t)lvl;
+        anch[AB[p] + (uint32_t)__popcll(rs & ((1ull << bb) - 1ull))] = (uint16_t)lvl;
         rsn &= rsn - 1ull;
       }
     };
@@ -283,6 +290,13 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
     uint16_t* D = A.dist + slot * A.dstride;
     const uint32_t Ww = (W + 31u) >> 5, nwords = A.H * Ww;
     const float invWw = 1.0f / (float)Ww;
+    // compact index of the anchor of run-start cell bit cb of block pb (bx & 3 = j): the block's
+    // run-start mask as in `anchors`
+    auto aidx = [&](uint32_t pb, uint32_t j, uint32_t cb) -> uint32_t {
+      const uint64_t f = FRs[pb];
+      const uint64_t wf = ((f << 1) & ~COL0) | (j ? ((FRs[pb - 1u] >> 7) & COL0) : 0ull);
+      return AB[pb] + (uint32_t)__popcll(f & ~wf & ((1ull << cb) - 1ull));
+    };
     // row word k -> (y, cw), its first block p0 and row-in-block r; bitmaps gathered from the 4
     // blocks' row bytes; the first 4 run anchors are loaded one iteration ahead (L2 latency)
     struct Word {
@@ -312,7 +326,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
 #pragma unroll
       for (uint32_t j = 0; j < 4u; ++j) {
         const uint32_t sj = rs ? (uint32_t)__builtin_ctz(rs) : 0u;
-        o.a[j] = ld_nc16(anch + (o.p0 + (sj >> 3)) * 64u + o.r * 8u + (sj & 7u));
+        o.a[j] = ld_nc16(anch + aidx(o.p0 + (sj >> 3), sj >> 3, o.r * 8u + (sj & 7u)));
         rs &= rs - 1u;
       }
     };
@@ -335,7 +349,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         for (uint32_t j = 5; rs != 0u; ++j) {
           const uint32_t sj = __builtin_ctz(rs);
           rs &= rs - 1u;
-          const uint32_t Aj = ld_nc16(anch + (p0 + (sj >> 3)) * 64u + r * 8u + (sj & 7u));
+          const uint32_t Aj = ld_nc16(anch + aidx(p0 + (sj >> 3), sj >> 3, r * 8u + (sj & 7u)));
           const uint32_t Fs = 2u * __popc(wl & (0xFFFFFFFFu >> (31u - sj))) - (sj + 1u);
           LS[ct_slot(lane, j)] = (uint16_t)(Aj - Fs);
         }
@@ -399,7 +413,7 @@ uint32_t bfs_blk_klog(uint32_t nbp) {
 
 uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds) {
   const size_t per_wave = (size_t)blk_bfs_words(nbp, 1u << bfs_blk_klog(nbp), cap) * 4u;
-  const size_t shared = (size_t)nbp * 8u;
+  const size_t shared = (size_t)(nbp + (nbp + 1u) / 2u) * 8u;  // FR u64 + AB u32
   if (max_lds <= 0 || shared + per_wave > (size_t)max_lds) return 0;
   return (uint32_t)std::min<size_t>(16u, ((size_t)max_lds - shared) / per_wave);
 }
@@ -410,7 +424,7 @@ hipError_t launch_bfs_blk(const BlkBfsArgs& A0, int max_lds, int num_cu, hipStre
   A.klog = bfs_blk_klog(A.nbp);
   A.bp_magic = (uint32_t)((0xFFFFFFFFull + A.Bp) / A.Bp);  // ceil(2^32 / Bp): exact p / Bp for p*Bp < 2^32
   const size_t per_wave = (size_t)blk_bfs_words(A.nbp, 1u << A.klog, A.cap) * 4u;
-  const size_t shared = (size_t)A.nbp * 8u;
+  const size_t shared = (size_t)(A.nbp + (A.nbp + 1u) / 2u) * 8u;  // FR u64 + AB u32
   const uint32_t nwv = std::min<uint32_t>(A.max_waves, bfs_blk_waves_per_block(A.nbp, A.cap, max_lds));
   if (nwv == 0 || A.nbp > 0x10000u || A.cap > 0x8000u) return hipErrorInvalidValue;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cu, (A.k + nwv - 1u) / nwv));

@@ -58,6 +58,8 @@ struct tsw_ctx {
   // K1 v3 (k_bfs_blk) 8x8-block grid
   uint32_t BW = 0, BH = 0, Bp = 0, nbp = 0, blk_cap = 576;
   uint64_t* d_frb = nullptr;
+  uint32_t* d_abase = nullptr;  // k_bfs_blk run-start numbering
+  uint32_t nrs = 0;
   unsigned long long* d_wlg = nullptr;  // k_bfs_blk per-wave WL scratch
   uint64_t wlg_waves = 0;
   uint16_t* d_anch = nullptr;
@@ -432,7 +434,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   if (nbw == 0 && c->bfs_mode == 3) RET(TSW_EINVAL, "k_bfs_blk does not fit this grid (TSW_BFS_KERNEL=blk)");
   if (nbw > 0) {
     Timer t(c, CAT_BFS);
-    TRY(ensure_wave_scratch(c, (uint64_t)c->num_cu * nbw, (size_t)c->nbp * 64u, (size_t)c->nbp * 2u));
+    TRY(ensure_wave_scratch(c, (uint64_t)c->num_cu * nbw, std::max<size_t>(c->nrs, 1), (size_t)c->nbp * 2u));
     if (c->wlg_waves < c->wave_scratch) {
       HIPCHK(hipStreamSynchronize(c->s));
       if (c->d_wlg) HIPCHK(hipFree(c->d_wlg));
@@ -450,6 +452,8 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     A.nbp = c->nbp;
     A.cap = c->blk_cap;
     A.frb = c->d_frb;
+    A.abase = c->d_abase;
+    A.nrs = c->nrs;
     A.goals = goals;
     A.slots = slots;
     A.k = k;
@@ -881,6 +885,21 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
       for (uint32_t x = 0; x < w; ++x)
         if (c->h_nbmask[(size_t)y * w + x] & NB_FREE)
           frb[(size_t)((y >> 3) + 1u) * c->Bp + (x >> 3)] |= 1ull << (((y & 7u) << 3) | (x & 7u));
+    // run starts (free cells whose west is blocked or x % 32 == 0) numbered in block order
+    std::vector<uint32_t> abase(c->nbp, 0u);
+    uint64_t nrs = 0;
+    for (uint32_t p = 0; p < c->nbp; ++p) {
+      const uint32_t bx = p % c->Bp;
+      const uint64_t f = frb[p], fw = p ? frb[p - 1u] : 0ull;
+      const uint64_t col0 = 0x0101010101010101ull;
+      const uint64_t wf = ((f << 1) & ~col0) | ((bx & 3u) ? ((fw >> 7) & col0) : 0ull);
+      abase[p] = (uint32_t)nrs;
+      nrs += (uint64_t)__builtin_popcountll(f & ~wf);
+    }
+    c->nrs = (uint32_t)nrs;
+    if ((e = hipMalloc(&c->d_abase, (size_t)c->nbp * 4)) != hipSuccess) return fail("malloc abase", e);
+    if ((e = hipMemcpy(c->d_abase, abase.data(), (size_t)c->nbp * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      return fail("copy abase", e);
     if ((e = hipMalloc(&c->d_frb, (size_t)c->nbp * 8)) != hipSuccess) return fail("malloc frb", e);
     if ((e = hipMemcpy(c->d_frb, frb.data(), (size_t)c->nbp * 8, hipMemcpyHostToDevice)) != hipSuccess)
       return fail("copy frb", e);
@@ -920,7 +939,7 @@ void tsw_destroy(tsw_ctx* c) {
   auto fre = [](void* p) {
     if (p) (void)hipFree(p);
   };
-  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_frb); fre(c->d_wlg); fre(c->d_anch); fre(c->d_lovf); fre(c->d_bprof); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
+  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_frb); fre(c->d_abase); fre(c->d_wlg); fre(c->d_anch); fre(c->d_lovf); fre(c->d_bprof); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
   fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);

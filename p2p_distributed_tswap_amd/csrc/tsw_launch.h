@@ -48,7 +48,9 @@ struct BlkBfsArgs {
   uint32_t k;
   uint16_t* dist;
   uint64_t dstride;
-  uint16_t* anch;         // per-wave anchor scratch, nbp * 64 u16 each
+  const uint32_t* abase;  // [nbp] index of the first run start of block p (run starts in block order)
+  uint32_t nrs;           // run starts in the grid
+  uint16_t* anch;         // per-wave compact anchor scratch, nrs u16 each
   uint16_t* lovf;         // per-wave list overflow, 2 * nbp u16 each
   unsigned long long* wlg;  // per-wave west-step blocks, nbp u64 each
   uint32_t* work;         // goal dequeue counter (zeroed before the launch)
