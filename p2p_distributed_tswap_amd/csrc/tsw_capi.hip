@@ -84,6 +84,7 @@ struct tsw_ctx {
   uint32_t* d_gs = nullptr;
   uint32_t* d_epochs = nullptr;
   uint32_t nslots16 = 0;  // LDS-heap A* (small grids)
+  uint32_t wave_hcap = 0;  // k_astar_wave LDS heap entries (0: default; TSW_ASTAR_WAVE_HCAP, tests)
   uint16_t* d_gs16 = nullptr;
   uint32_t* d_ep16 = nullptr;
   AstarQuery* d_ovf = nullptr;
@@ -343,8 +344,21 @@ int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint
       HIPCHK(launch_astar(c->G, c->d_ovf, nullptr, novf, novf, nh, c->tstride, res, lens, c->d_heaps, c->hcap,
                           c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
   } else {
-    HIPCHK(launch_astar(c->G, Q, nullptr, nq, nq, nh, c->tstride, res, lens, c->d_heaps, c->hcap, c->d_gs,
-                        c->d_epochs, c->nslots, &c->d_stat->err, c->s));
+    // one query per wave, LDS heap; the g_score slots are shared with k_astar (same tag scheme)
+    if (nq > c->ovf_cap) {
+      HIPCHK(hipStreamSynchronize(c->s));
+      HIPCHK(dgrow(c->d_ovf, c->ovf_cap, nq));
+    }
+    HIPCHK(hipMemsetAsync(&c->d_stat->novf, 0, 4, c->s));
+    const uint32_t slots = std::min(astar_wave_slots(c->G, c->num_cu), c->nslots);
+    HIPCHK(launch_astar_wave(c->G, Q, nq, nh, c->tstride, res, lens, c->d_gs, c->d_epochs, slots, c->d_ovf,
+                             &c->d_stat->novf, c->wave_hcap, c->s));
+    HIPCHK(hipMemcpyAsync(&c->h_stat->novf, &c->d_stat->novf, 4, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    const uint32_t novf = c->h_stat->novf;
+    if (novf)
+      HIPCHK(launch_astar(c->G, c->d_ovf, nullptr, novf, novf, nh, c->tstride, res, lens, c->d_heaps, c->hcap,
+                          c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
   }
   c->st.astar_queries += nq;
   c->st.astar_launches++;
@@ -627,6 +641,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.occ = c->d_occ;
   P.mu = c->d_mu;
   P.has_dups = *c->h_dups;
+  P.prefetch = getenv("TSW_NO_PREFETCH") ? 0u : 1u;
   P.pick_xy = c->d_pick_xy;
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;
@@ -906,6 +921,7 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
     if (const char* m = getenv("TSW_BFS_KERNEL"))
       c->bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : !strcmp(m, "blk") ? 3u : 0u;
     if (const char* m = getenv("TSW_BFS_LISTCAP")) c->bfs_cap = std::max(1, std::min(atoi(m), 32768));
+    if (const char* m = getenv("TSW_ASTAR_WAVE_HCAP")) c->wave_hcap = (uint32_t)std::max(4, atoi(m));
     if (const char* m = getenv("TSW_BFS_BLKCAP")) c->blk_cap = std::max(1, std::min(atoi(m), 32768));
   }
   c->h_goal_tab.assign(ncell, -1);

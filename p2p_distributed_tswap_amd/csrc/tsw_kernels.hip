@@ -14,6 +14,8 @@
 // Launch wrappers are plain C++ functions declared in tsw_launch.h.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "tsw_internal.h"
 #include "tsw_launch.h"
 
@@ -280,8 +282,10 @@ __device__ __forceinline__ uint64_t heap_pop(uint64_t* Hp, uint32_t& len) {
   return top;
 }
 
-__device__ uint8_t astar_one(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag, uint64_t* Hp,
-                             uint32_t hcap, uint32_t* GS, int32_t* len_out, uint32_t* err) {
+// err == nullptr: a heap overflow returns NH_UNKNOWN with *len_out = -2 (caller re-queues the
+// query to a larger heap) instead of raising ERR_HEAP_OVERFLOW.
+__device__ __forceinline__ uint8_t astar_one(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag, uint64_t* Hp,
+                                             uint32_t hcap, uint32_t* GS, int32_t* len_out, uint32_t* err) {
   const uint32_t W = G.W;
   const uint32_t vx = v % W, vy = v / W, gx = goal % W, gy = goal / W;
   if (v == goal) {
@@ -320,8 +324,8 @@ __device__ uint8_t astar_one(const DevGrid& G, uint32_t v, uint32_t goal, uint32
         const uint32_t lab = cg == 0 ? d : labc;
         GS[nc] = tagw | (lab << 20) | tg;
         if (len >= hcap) {
-          atomicOr(err, ERR_HEAP_OVERFLOW);
-          *len_out = -1;
+          if (err) atomicOr(err, ERR_HEAP_OVERFLOW);
+          *len_out = err ? -1 : -2;
           return NH_UNKNOWN;
         }
         const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
@@ -492,6 +496,117 @@ __global__ void __launch_bounds__(64) k_astar(DevGrid G, const AstarQuery* __res
   epochs[slot] = ep;
 }
 
+// astar_one with a BYTE g_score per cell (LDS-resident on grids of up to ~120k cells):
+// bit 7 valid | label:2 | h:5 with g = manhattan(start, cell) + 2h (g and the Manhattan
+// distance from the start have the same parity on a 4-grid, and g >= it). A g that would
+// need h > 31, or a heap longer than hcap, returns NH_UNKNOWN with *len_out = -2 (the caller
+// hands the query to the u32 g_score kernel). Same heap, same relaxations, same labels.
+__device__ __forceinline__ uint8_t astar_one_b8(const DevGrid& G, uint32_t v, uint32_t goal, uint64_t* Hp,
+                                                uint32_t hcap, uint8_t* GB, int32_t* len_out) {
+  const uint32_t W = G.W;
+  const uint32_t vx = v % W, vy = v / W, gx = goal % W, gy = goal / W;
+  if (v == goal) {
+    *len_out = 1;
+    return NH_STAY;
+  }
+  uint32_t len = 0;
+  GB[v] = 0x80u;
+  {
+    const uint32_t h0 = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
+    Hp[0] = mk_entry(h0, 0, vx, vy);
+    len = 1;
+  }
+  while (len > 0) {
+    const uint64_t e = heap_pop(Hp, len);
+    const uint32_t cx = (uint32_t)(e >> 11) & 0x7FFu, cy = (uint32_t)e & 0x7FFu;
+    const uint32_t cg = (uint32_t)(e >> 22) & 0x1FFFFFu;
+    const uint32_t c = cy * W + cx;
+    if (c == goal) {
+      *len_out = (int32_t)cg + 1;
+      return (uint8_t)((GB[goal] >> 5) & 3u);
+    }
+    const uint8_t m = G.nbmask[c];
+    const uint32_t labc = (GB[c] >> 5) & 3u;
+    const uint32_t tg = cg + 1u;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+      if (!(m & (1u << d))) continue;
+      const uint32_t nx = d == 1 ? cx + 1 : (d == 3 ? cx - 1 : cx);
+      const uint32_t ny = d == 0 ? cy + 1 : (d == 2 ? cy - 1 : cy);
+      const uint32_t nc = ny * W + nx;
+      const uint32_t man = (nx > vx ? nx - vx : vx - nx) + (ny > vy ? ny - vy : vy - ny);
+      const uint32_t old = GB[nc];
+      const uint32_t oldg = (old & 0x80u) ? man + 2u * (old & 31u) : 0xFFFFFFFFu;
+      if (tg < oldg) {
+        const uint32_t hh = (tg - man) >> 1;
+        if (hh > 31u || len >= hcap) {
+          *len_out = -2;
+          return NH_UNKNOWN;
+        }
+        const uint32_t lab = cg == 0 ? d : labc;
+        GB[nc] = (uint8_t)(0x80u | (lab << 5) | hh);
+        const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
+        heap_sift_up(Hp, len, mk_entry(tg + h, tg, nx, ny));
+        ++len;
+      }
+    }
+  }
+  *len_out = 2;
+  return fallback_code(G.nbmask[v], vx, vy, gx, gy);
+}
+
+// ----------------------------------------------------------------------------
+// K3 (grids of > 1024 cells): the same exact A* (astar_one), ONE QUERY PER WAVE with the heap
+// in LDS and, when the grid fits (WAVE_GS_LDS_MAX cells), the g_score words in LDS too. The
+// planner's lazy mode exits to the host whenever a step needs unresolved next hops, so K3
+// runs in many small batches and its latency is the slowest query of a batch: a heap sift
+// step here is an LDS round trip instead of a dependent global load. Queries whose heap
+// outgrows the LDS heap go to the overflow list (k_astar, global-memory heap).
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* __restrict__ Q, uint32_t nq,
+                                                   uint8_t* __restrict__ nh_base, uint64_t nstride,
+                                                   uint8_t* __restrict__ res, int32_t* __restrict__ lens,
+                                                   uint32_t hcap, uint32_t gs_lds, uint32_t* __restrict__ gs_all,
+                                                   uint32_t* __restrict__ epochs, AstarQuery* __restrict__ ovf,
+                                                   uint32_t* __restrict__ novf) {
+  extern __shared__ __align__(16) uint64_t wsm[];
+  uint64_t* Hp = wsm;
+  const uint32_t lane = threadIdx.x, ncell = G.ncell;
+  // gs_lds: 0 = u32 g_scores in global slots, 1 = u32 in LDS, 2 = bytes in LDS (astar_one_b8)
+  uint32_t* GS = gs_lds == 1u ? reinterpret_cast<uint32_t*>(wsm + hcap) : gs_all + (uint64_t)blockIdx.x * ncell;
+  uint8_t* GB = reinterpret_cast<uint8_t*>(wsm + hcap);
+  uint32_t ep = gs_lds ? 0u : epochs[blockIdx.x];
+  if (gs_lds == 1u)
+    for (uint32_t c = lane; c < ncell; c += 64u) GS[c] = 0u;
+  __syncthreads();
+  for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    if (gs_lds == 2u) {
+      uint4* g4 = reinterpret_cast<uint4*>(GB);
+      for (uint32_t c = lane; c < (ncell + 15u) / 16u; c += 64u) g4[c] = make_uint4(0u, 0u, 0u, 0u);
+    } else if (ep % 1023u == 0u && ep > 0u) {
+      for (uint32_t c = lane; c < ncell; c += 64u) GS[c] = 0u;
+      __threadfence_block();
+    }
+    __syncthreads();
+    const uint32_t tag = ep % 1023u + 1u;
+    ++ep;
+    if (lane == 0) {
+      const AstarQuery q = Q[qi];
+      int32_t L = 0;
+      const uint8_t code = gs_lds == 2u ? astar_one_b8(G, q.v, q.goal, Hp, hcap, GB, &L)
+                                        : astar_one(G, q.v, q.goal, tag, Hp, hcap, GS, &L, nullptr);
+      if (L == -2) {
+        ovf[atomicAdd(novf, 1u)] = q;  // heap outgrew LDS: resolved by k_astar
+      } else {
+        if (res) res[q.out] = code;
+        if (lens) lens[q.out] = L;
+        if (nh_base && q.tab >= 0) nh_base[(uint64_t)q.tab * nstride + q.v] = code;
+      }
+    }
+  }
+  if (!gs_lds && lane == 0) epochs[blockIdx.x] = ep;
+}
+
 // Enqueue every unresolved (goal, cell) of the given table slots (eager mode).
 __global__ void k_enqueue_unknown(DevGrid G, const uint32_t* __restrict__ goals,
                                   const uint32_t* __restrict__ slots, uint32_t k,
@@ -590,6 +705,40 @@ hipError_t launch_astar_lds(const DevGrid& G, const AstarQuery* Q, uint32_t nq, 
 }
 
 bool astar_lds_ok(const DevGrid& G) { return G.ncell <= 1024u; }
+
+constexpr uint32_t WAVE_HCAP = 4096;              // LDS heap entries (32 KiB)
+constexpr uint32_t WAVE_GS_LDS_MAX = 24u * 1024u;   // cells whose u32 g_score words fit LDS beside it
+constexpr uint32_t WAVE_GB_LDS_MAX = 120u * 1024u;  // cells whose byte g_scores fit LDS beside it
+
+static uint32_t wave_gs_mode(const DevGrid& G) {
+  return G.ncell <= WAVE_GS_LDS_MAX ? 1u : G.ncell <= WAVE_GB_LDS_MAX ? 2u : 0u;
+}
+
+static size_t wave_lds_bytes(const DevGrid& G, uint32_t hcap) {
+  const uint32_t m = wave_gs_mode(G);
+  return (size_t)hcap * 8u + (m == 1u ? (size_t)G.ncell * 4u : m == 2u ? ((size_t)G.ncell + 15u) / 16u * 16u : 0u);
+}
+
+uint32_t astar_wave_slots(const DevGrid& G, int num_cu) {
+  const size_t lds = wave_lds_bytes(G, WAVE_HCAP);
+  const uint32_t per_cu = (uint32_t)std::max<size_t>(1, (160u * 1024u) / lds);
+  return (uint32_t)num_cu * std::min<uint32_t>(per_cu, 16u);
+}
+
+hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
+                             uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
+                             AstarQuery* ovf, uint32_t* novf, uint32_t hcap, hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  const uint32_t gs_lds = wave_gs_mode(G);
+  hcap = hcap ? std::max<uint32_t>(4u, std::min(hcap, WAVE_HCAP)) : WAVE_HCAP;
+  const size_t lds = wave_lds_bytes(G, hcap);
+  const uint32_t grid = std::min(nq, nslots);
+  hipError_t e = hipFuncSetAttribute((const void*)k_astar_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_astar_wave, dim3(grid), dim3(64), lds, s, G, Q, nq, nh_base, nstride, res, lens, hcap,
+                     gs_lds, gs_all, epochs, ovf, novf);
+  return hipGetLastError();
+}
 
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,

@@ -77,6 +77,13 @@ hipError_t launch_astar_lds(const DevGrid& G, const AstarQuery* Q, uint32_t nq, 
                             uint8_t* res, int32_t* lens, uint16_t* gs16, uint32_t* epochs, uint32_t nslots,
                             AstarQuery* ovf, uint32_t* novf, hipStream_t s);
 
+// One query per wave, LDS heap (grids of > 1024 cells); gs_all/epochs: nslots u32 g_score
+// arrays of ncell words (used only when the grid's g_scores do not fit LDS).
+uint32_t astar_wave_slots(const DevGrid& G, int num_cu);
+hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
+                             uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
+                             AstarQuery* ovf, uint32_t* novf, uint32_t hcap /*0: default*/, hipStream_t s);
+
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
                                   uint32_t qcap, hipStream_t s);

@@ -206,6 +206,29 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
   return *s_q;
 }
 
+// Parallel, after rules_init: the next hops a firing of this rules round could need. A rule-3
+// swap hands succ(k) the goal of k (tswap.rs:199-202); a rule-4 rotation hands every cycle
+// member the goal of its predecessor on the cycle (:241-249) — both are the pair
+// (cell of succ(k), goal of k) for a firing candidate k. Enqueuing every unresolved such pair
+// up front turns what would be one planner exit per firing into one batched K3 launch.
+// Returns the number of enqueued pairs (block-uniform).
+__device__ uint32_t rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  if (tid == 0) *s_q = 0;
+  __syncthreads();
+  for (uint32_t k = tid; k < P.n; k += bd) {
+    const uint32_t s = S.SUCC[k];
+    if (s == SUCC_TERM || s == k) continue;
+    if (!(S.ONC[k] || S.V[s] == S.G[s])) continue;
+    const int32_t tab = S.GT[k];
+    if (tab < 0) continue;
+    const uint32_t vs = S.V[s];
+    if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) enqueue_pair(P, vs, S.G[k], tab, s_q);
+  }
+  __syncthreads();
+  return *s_q;
+}
+
 // Serial movement phase (tswap.rs:257-285) — used when cells are shared by several agents
 // (duplicate start cells); false on an unresolved next hop.
 __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
@@ -477,6 +500,18 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // one through s. CANDC[k] prefetches s's next hop toward k's goal for every rule-3
       // candidate k, so a swap needs no global round trip on the serial path.
       rules_init(P, S);
+      if (P.prefetch) {
+        const uint32_t q0 = rules_prefetch(P, S, &s_q);
+        if (q0 > 0) {
+          if (tid == 0) {
+            s_ctl.qcount = q0;
+            s_ctl.status = PLAN_NEED_QUERIES;
+            s_exit = 1;
+          }
+          __syncthreads();
+          break;
+        }
+      }
       for (;;) {
         const uint32_t cursor = s_ctl.i;
         uint32_t best = NO_AGENT;
@@ -567,6 +602,18 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             break;
           }
           rules_init(P, S);
+          if (P.prefetch) {
+            const uint32_t q1 = rules_prefetch(P, S, &s_q);
+            if (q1 > 0) {
+              if (tid == 0) {
+                s_ctl.qcount = q1;
+                s_ctl.status = PLAN_NEED_QUERIES;
+                s_exit = 1;
+              }
+              __syncthreads();
+              break;
+            }
+          }
         }
       }
       if (s_exit) break;

@@ -1,0 +1,95 @@
+"""End-to-end MAPD planning at scale on one GPU vs the single-thread CPU restatement.
+
+north_star: "a 10k-agent warehouse instance planned end-to-end faster than the host-CPU reference".
+For each instance: the GPU plans the full horizon (cap 2000) from an empty table store (K1 BFS
+tables + next-hop resolution + every timestep on the device) and is timed end to end; the CPU
+oracle (oracle/tswap_oracle.c, -O2, one thread — the checker, used here only as the timed
+baseline) plans a bounded PREFIX of timesteps, is timed, and its prefix is compared bit-exactly
+with the GPU's. CPU whole-plan time is extrapolated from the prefix rate (labelled as such).
+
+usage: python scripts/scale_bench.py [instance ...] [--cpu-steps N]
+instances: c3 (warehouse 170x84, 1,000 agents, 3,000 tasks — BASELINE configs[2]),
+           wh10k (warehouse 510x220, 10,000 agents, 30,000 tasks)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+from p2p_distributed_tswap_amd import Planner, maps  # noqa: E402
+
+# name: (map factory, agents, tasks, seed, CPU prefix timesteps)
+INSTANCES = {
+    "c3": (lambda: maps.warehouse_map(170, 84, 0x170084), 1000, 3000, 0x170084, 20),
+    "wh10k": (lambda: maps.warehouse_map(510, 220, 0x510220), 10000, 30000, 0x510220, 3),
+}
+
+
+def _heartbeat(stop, t0):
+    """A long plan is one blocking C call: print progress so a batch runner sees it is alive."""
+    while not stop.wait(30.0):
+        print(f"[scale_bench] still planning, {time.perf_counter() - t0:.0f} s", flush=True)
+
+
+def main():
+    import threading
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("instances", nargs="*", default=["c3", "wh10k"])
+    ap.add_argument("--cpu-steps", type=int, default=0, help="CPU prefix timesteps (0: per-instance default)")
+    ap.add_argument("--max-t", type=int, default=2000)
+    args = ap.parse_args()
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleGraph  # CPU baseline + prefix check only
+
+    for name in args.instances:
+        fac, n, m, seed, cpu_steps = INSTANCES[name]
+        cpu_steps = args.cpu_steps or cpu_steps
+        rows = fac()
+        h, w = len(rows), len(rows[0])
+        starts, tasks = maps.make_instance(rows, n, m, seed)
+        with Planner(rows) as p:
+            p.plan_mapd_arrays(starts[:8], tasks[:8], 4)  # context warm-up (not timed)
+            p.clear_tables()
+            p.reset_stats()
+            t0 = time.perf_counter()
+            stop = threading.Event()
+            hb = threading.Thread(target=_heartbeat, args=(stop, t0), daemon=True)
+            hb.start()
+            try:
+                rec, _ = p.plan_mapd_arrays(starts, tasks, args.max_t)
+            finally:
+                stop.set()
+            gpu_s = time.perf_counter() - t0
+            st = p.stats()
+        T = rec.shape[1]
+        og = OracleGraph(maps.rows_to_array(rows))
+        tc = time.perf_counter()
+        crec, _ = og.mapd(starts, tasks, cpu_steps)
+        cpu_s = time.perf_counter() - tc
+        ct = crec.shape[1]
+        prefix_ok = bool(np.array_equal(crec, rec[:, :ct]))
+        cpu_rate = n * ct / cpu_s
+        out = {
+            "instance": name, "grid": f"{w}x{h}", "agents": n, "tasks": m, "timesteps": int(T),
+            "gpu_end_to_end_s": round(gpu_s, 3), "gpu_agent_steps_per_s": round(n * T / gpu_s, 1),
+            "cpu_prefix_timesteps": int(ct), "cpu_prefix_s": round(cpu_s, 3),
+            "cpu_agent_steps_per_s": round(cpu_rate, 1),
+            "cpu_end_to_end_s_extrapolated": round(n * T / cpu_rate, 1),
+            "speedup_end_to_end": round((n * T / cpu_rate) / gpu_s, 1),
+            "prefix_bit_exact": prefix_ok,
+            "tables": st["tables"], "bfs_ms": round(st["bfs_ms"], 2), "astar_ms": round(st["astar_ms"], 2),
+            "plan_ms": round(st["plan_ms"], 2), "astar_queries": st["astar_queries"],
+            "astar_launches": st["astar_launches"], "plan_launches": st["walker_launches"],
+            "plan_section_ms": [round(x, 2) for x in st["plan_section_ms"]],
+        }
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -21,6 +21,14 @@ def _grid(name):
         return maps.warehouse_map(170, 84, 0x170084)
     if name == "cave":
         return maps.cave_map(256, 257, 0x520D)
+    if name == "serpentine":
+        # 200x130 (> 24k cells: byte g-score A*): walls every 4th column with alternating end
+        # gaps, so paths detour far beyond the Manhattan distance (exercises the h > 31 hand-off)
+        a = np.zeros((130, 200), dtype=bool)
+        for i, x in enumerate(range(3, 200, 4)):
+            a[:, x] = True
+            a[(1 if i % 2 else 128), x] = False
+        return maps.to_rows(a)
     raise KeyError(name)
 
 
@@ -52,7 +60,8 @@ def test_astar_all_pairs_open8():
         assert (nxt[q], ln[q]) == (rn, rl), f"query {s[q]}->{g[q]}"
 
 
-@pytest.mark.parametrize("name,nq", [("rand16", 2000), ("rand32", 4000), ("bundled", 1500), ("warehouse", 800)])
+@pytest.mark.parametrize("name,nq", [("rand16", 2000), ("rand32", 4000), ("bundled", 1500), ("warehouse", 800),
+                                     ("cave", 300), ("serpentine", 200)])
 def test_astar_random_pairs(name, nq):
     rows = _grid(name)
     cells = maps.rows_to_array(rows)
@@ -69,6 +78,25 @@ def test_astar_random_pairs(name, nq):
         if (nxt[q], ln[q]) != (rn, rl):
             bad.append((int(s[q]), int(g[q]), int(nxt[q]), int(ln[q]), rn, rl))
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("name", ["warehouse", "cave"])
+def test_astar_wave_heap_overflow_handoff(monkeypatch, name):
+    """k_astar_wave (grids > 1024 cells) with a tiny LDS heap (read at context creation): queries
+    that outgrow it are handed to the global-heap kernel; results stay bit-exact."""
+    rows = _grid(name)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@"))
+    rng = np.random.default_rng(5)
+    s = rng.choice(free, 200).astype(np.uint32)
+    g = rng.choice(free, 200).astype(np.uint32)
+    monkeypatch.setenv("TSW_ASTAR_WAVE_HCAP", "16")
+    with Planner(rows) as p:
+        nxt, ln = p.get_path_next(s, g)
+    for q in range(s.size):
+        rn, rl, _ = og.get_path_next(int(s[q]), int(g[q]))
+        assert (nxt[q], ln[q]) == (rn, rl), f"query {s[q]}->{g[q]}"
 
 
 @pytest.mark.parametrize("name,n,seed", [("rand16", 40, 1), ("rand32", 200, 2), ("bundled", 60, 3),
@@ -98,6 +126,7 @@ def test_step_matches_oracle(name, n, seed):
     ("rand32", 200, 600, 0x3232, 0),
     ("rand32", 120, 300, 5, TSW_F_LAZY_NEXTHOP),
     ("bundled", 10, 30, 1, 0),
+    ("warehouse", 100, 300, 9, 0),
 ])
 def test_mapd_matches_oracle(name, n, m, seed, flags):
     rows = _grid(name)
