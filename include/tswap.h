@@ -150,6 +150,9 @@ typedef struct {
      * [5] record [6] done/other [7] launch copy-in/out */
     double plan_section_ms[8];
     uint64_t rule_rounds;       /* first-firing rounds run by the rules phase */
+    /* plan-kernel exits for K3 next-hop resolution, by the section that needed the codes
+     * (same indices as plan_section_ms; [7] = relaunch entry) */
+    uint64_t plan_exits[8];
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

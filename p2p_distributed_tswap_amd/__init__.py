@@ -85,11 +85,13 @@ class Stats(ctypes.Structure):
         ("assign_launches", ctypes.c_uint64), ("assign_ms", ctypes.c_double),
         ("steps", ctypes.c_uint64), ("tables", ctypes.c_uint64), ("plan_ms", ctypes.c_double),
         ("plan_section_ms", ctypes.c_double * 8), ("rule_rounds", ctypes.c_uint64),
+        ("plan_exits", ctypes.c_uint64 * 8),
     ]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
         d["plan_section_ms"] = list(self.plan_section_ms)
+        d["plan_exits"] = list(self.plan_exits)
         return d
 
 

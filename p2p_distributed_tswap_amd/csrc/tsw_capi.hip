@@ -700,10 +700,18 @@ int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     if (k.status == PLAN_DONE) {
       c->chase_id = k.chase_id;
       c->st.rule_rounds += k.rule_rounds;
+      // pairs the rules prefetch queued but no firing needed: resolve them so no table entry
+      // is left PENDING for later calls
+      if (k.qcount > 0) {
+        if (k.qcount > P.qcap) RET(TSW_EINVAL, "plan kernel queue overflow");
+        TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
+        TRY(check_err(c));
+      }
       return TSW_OK;
     }
     if (k.status != PLAN_NEED_QUERIES || k.qcount == 0 || k.qcount > P.qcap)
       RET(TSW_EINVAL, "plan kernel stopped without resolvable next hops");
+    c->st.plan_exits[std::min<uint32_t>(k.section, 7u)]++;
     TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
     TRY(check_err(c));
   }
@@ -770,7 +778,7 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   HIPCHK(hipStreamSynchronize(c->s));  // host vectors above go out of scope only at return, but keep it simple
   TRY(build_occ(c, n));
   TRY(ensure_tables(c, goalset));
-  TRY(ensure_queue(c, std::max<size_t>(n, 64)));
+  TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
   PlanArgs P = plan_args(c, n, m, MODE_MAPD, goal_out != nullptr);
   PlanCtl init{};
   init.section = SEC_ASSIGN;
@@ -1004,7 +1012,7 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   HIPCHK(hipMemcpyAsync(c->d_g, g, n * 4ull, hipMemcpyHostToDevice, c->s));
   TRY(build_occ(c, n));
   TRY(ensure_tables(c, goals));
-  TRY(ensure_queue(c, std::max<size_t>(n, 64)));
+  TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
   PlanArgs P = plan_args(c, n, 0, MODE_STEP, false);
   PlanCtl init{};
   init.section = SEC_PRE1;

@@ -184,10 +184,12 @@ __device__ __forceinline__ uint32_t enqueue_pair(const PlanArgs& P, uint32_t v, 
 }
 
 // parallel: refresh next-hop codes of agents whose code is dirty; unresolved pairs are
-// enqueued for K3. Returns the number of enqueued pairs (block-uniform).
-__device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
+// appended to the launch's K3 queue (s_q counts every pair queued since the launch began,
+// speculative prefetches included). Returns how many dirty agents still lack a code
+// (block-uniform): the planner must exit for K3 iff that is nonzero.
+__device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
-  if (tid == 0) *s_q = 0;
+  if (tid == 0) *s_need = 0;
   __syncthreads();
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (S.NHC[k] <= NH_STAY) continue;
@@ -199,34 +201,46 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
       continue;
     }
     const uint8_t code = P.nh[(uint64_t)tab * P.nstride + v];
-    if (code <= NH_STAY) S.NHC[k] = code;
-    else enqueue_pair(P, v, g, tab, s_q);
+    if (code <= NH_STAY) {
+      S.NHC[k] = code;
+    } else {
+      enqueue_pair(P, v, g, tab, s_q);  // no-op if already queued (PENDING)
+      atomicAdd(s_need, 1u);
+    }
   }
   __syncthreads();
-  return *s_q;
+  return *s_need;
 }
 
-// Parallel, after rules_init: the next hops a firing of this rules round could need. A rule-3
+// Parallel, after rules_init: the next hops a firing of this rules round (or the movement phase
+// after it) could need. A rule-3
 // swap hands succ(k) the goal of k (tswap.rs:199-202); a rule-4 rotation hands every cycle
 // member the goal of its predecessor on the cycle (:241-249) — both are the pair
-// (cell of succ(k), goal of k) for a firing candidate k. Enqueuing every unresolved such pair
-// up front turns what would be one planner exit per firing into one batched K3 launch.
-// Returns the number of enqueued pairs (block-uniform).
-__device__ uint32_t rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
+// (cell of succ(k), goal of k) for a firing candidate k. Every unresolved such pair is queued
+// speculatively (no exit): the planner exits only when a firing actually needs a code, and
+// that one K3 launch then resolves everything queued so far. Half the queue stays free for the
+// pairs an exit needs.
+__device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
-  if (tid == 0) *s_q = 0;
-  __syncthreads();
   for (uint32_t k = tid; k < P.n; k += bd) {
+    if (*(volatile uint32_t*)s_q >= P.qcap / 2u) break;
+    const int32_t tab = S.GT[k];
+    if (tab < 0) continue;
+    // k's own next hop from the cell it moves to: read by the movement phase when k moved
+    // earlier in the same step (tswap.rs:263-273, later agents see earlier moves) and by the
+    // next step's refresh
+    const uint8_t c = S.NHC[k];
+    if (c < NH_STAY && S.V[k] != S.G[k]) {
+      const uint32_t u = step_cell(S.V[k], c, P.W);
+      if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) enqueue_pair(P, u, S.G[k], tab, s_q);
+    }
     const uint32_t s = S.SUCC[k];
     if (s == SUCC_TERM || s == k) continue;
     if (!(S.ONC[k] || S.V[s] == S.G[s])) continue;
-    const int32_t tab = S.GT[k];
-    if (tab < 0) continue;
     const uint32_t vs = S.V[s];
     if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) enqueue_pair(P, vs, S.G[k], tab, s_q);
   }
   __syncthreads();
-  return *s_q;
 }
 
 // Serial movement phase (tswap.rs:257-285) — used when cells are shared by several agents
@@ -284,7 +298,7 @@ template <bool AG, bool OC>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss;
+  __shared__ uint32_t s_q, s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[8], s_tlast;
@@ -359,6 +373,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_ctl = *P.ctl;
     s_ctl.status = PLAN_RUNNING;
     s_exit = 0;
+    s_q = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     for (int k = 0; k < 8; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
@@ -366,9 +381,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   __syncthreads();
   if (s_ctl.section == SEC_RULES || s_ctl.section == SEC_MOVE) {
     // resuming after K3 resolved the missing next hops: every code starts dirty here
-    const uint32_t q = refresh_codes(P, S, &s_q);
+    const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
     if (q > 0 && tid == 0) {
-      s_ctl.qcount = q;
+      s_ctl.qcount = s_q;
       s_ctl.status = PLAN_NEED_QUERIES;
       s_exit = 1;
     }
@@ -476,10 +491,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       }
       __syncthreads();
     } else if (sec == SEC_PRE1 || sec == SEC_PRE2) {
-      const uint32_t q = refresh_codes(P, S, &s_q);
+      const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
       if (q > 0) {
         if (tid == 0) {
-          s_ctl.qcount = q;
+          s_ctl.qcount = s_q;
           s_ctl.status = PLAN_NEED_QUERIES;
           s_exit = 1;
         }
@@ -500,18 +515,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // one through s. CANDC[k] prefetches s's next hop toward k's goal for every rule-3
       // candidate k, so a swap needs no global round trip on the serial path.
       rules_init(P, S);
-      if (P.prefetch) {
-        const uint32_t q0 = rules_prefetch(P, S, &s_q);
-        if (q0 > 0) {
-          if (tid == 0) {
-            s_ctl.qcount = q0;
-            s_ctl.status = PLAN_NEED_QUERIES;
-            s_exit = 1;
-          }
-          __syncthreads();
-          break;
-        }
-      }
+      if (P.prefetch) rules_prefetch(P, S, &s_q);
       for (;;) {
         const uint32_t cursor = s_ctl.i;
         uint32_t best = NO_AGENT;
@@ -591,10 +595,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (s_best == NO_AGENT) break;
         if (s_miss) {
           // goals of the fired agents changed: their next hops (hence succ) must be looked up
-          const uint32_t q = refresh_codes(P, S, &s_q);
+          const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
           if (q > 0) {
             if (tid == 0) {
-              s_ctl.qcount = q;
+              s_ctl.qcount = s_q;
               s_ctl.status = PLAN_NEED_QUERIES;
               s_exit = 1;
             }
@@ -602,18 +606,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             break;
           }
           rules_init(P, S);
-          if (P.prefetch) {
-            const uint32_t q1 = rules_prefetch(P, S, &s_q);
-            if (q1 > 0) {
-              if (tid == 0) {
-                s_ctl.qcount = q1;
-                s_ctl.status = PLAN_NEED_QUERIES;
-                s_exit = 1;
-              }
-              __syncthreads();
-              break;
-            }
-          }
+          if (P.prefetch) rules_prefetch(P, S, &s_q);
         }
       }
       if (s_exit) break;
@@ -633,10 +626,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       }
       __syncthreads();
       if (s_ctl.miss) {
-        const uint32_t q = refresh_codes(P, S, &s_q);
+        const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
         if (tid == 0) {
-          s_ctl.qcount = q;
-          s_ctl.status = (q > 0 && s_ctl.miss == 1) ? PLAN_NEED_QUERIES : PLAN_ERROR;
+          s_ctl.qcount = s_q;
+          s_ctl.status = (q > 0 && s_q > 0 && s_ctl.miss == 1) ? PLAN_NEED_QUERIES : PLAN_ERROR;
           s_exit = 1;
         }
         __syncthreads();
@@ -650,10 +643,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (tid == 0) s_ctl.i = 1;  // DEC initialised for this step (survives relaunches)
       }
       for (;;) {
-        if (tid == 0) {
-          s_q = 0;
-          s_miss = 0;
-        }
+        if (tid == 0) s_miss = 0;
         __syncthreads();
         // A: target cell of every open agent; reset MU at its target and its own cell
         int open = 0;
@@ -780,6 +770,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (tid == 0) {
           s_ctl.status = PLAN_DONE;
           s_ctl.section = SEC_DONE;
+          s_ctl.qcount = s_q;  // speculative prefetches still queued: the host resolves them
           s_exit = 1;
         }
         __syncthreads();
@@ -808,6 +799,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if ((s_ctl.unused == 0u && !busy) || s_ctl.t > s_ctl.max_t) {
           s_ctl.status = PLAN_DONE;
           s_ctl.section = SEC_DONE;
+          s_ctl.qcount = s_q;  // speculative prefetches still queued: the host resolves them
           s_exit = 1;
         } else {
           s_ctl.section = SEC_ASSIGN;

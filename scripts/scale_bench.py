@@ -87,6 +87,7 @@ def main():
             "plan_ms": round(st["plan_ms"], 2), "astar_queries": st["astar_queries"],
             "astar_launches": st["astar_launches"], "plan_launches": st["walker_launches"],
             "plan_section_ms": [round(x, 2) for x in st["plan_section_ms"]],
+            "plan_exits_by_section": st["plan_exits"], "rule_rounds": st["rule_rounds"],
         }
         print(json.dumps(out), flush=True)
 
