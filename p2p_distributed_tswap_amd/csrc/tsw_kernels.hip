@@ -556,6 +556,128 @@ __device__ __forceinline__ uint8_t astar_one_b8(const DevGrid& G, uint32_t v, ui
 }
 
 // ----------------------------------------------------------------------------
+// Single-lane A* core for k_astar_wave. A lone lane is instruction-bound, so the heap entry
+// keeps its ORDER KEY in the high dword: (f << 15 | g) << 32 | x << 16 | y — one 32-bit
+// compare per sift step and no division to recover (x, y). Same order as mk_entry's key
+// (f, then g; cell bits never compared). f >= 2^17 or g >= 2^15 hands the query off (-2).
+// GSM 0/1: u32 tag | label | g words (global slot / LDS); GSM 2: byte words as astar_one_b8.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t hk(uint64_t e) { return (uint32_t)(e >> 32); }
+
+__device__ __forceinline__ void hk_sift_up(uint64_t* Hp, uint32_t pos, uint64_t elem) {
+  const uint32_t k = hk(elem);
+  while (pos > 0) {
+    const uint32_t parent = (pos - 1u) >> 1;
+    const uint64_t pe = Hp[parent];
+    if (k >= hk(pe)) break;  // elem <= parent
+    Hp[pos] = pe;
+    pos = parent;
+  }
+  Hp[pos] = elem;
+}
+
+__device__ __forceinline__ uint64_t hk_pop(uint64_t* Hp, uint32_t& len) {
+  const uint32_t end = --len;
+  const uint64_t last = Hp[end];
+  if (end == 0) return last;
+  const uint64_t top = Hp[0];
+  uint32_t pos = 0, child = 1;
+  while (child + 1u < end) {
+    uint64_t l = Hp[child];
+    const uint64_t r = Hp[child + 1];
+    if (hk(l) >= hk(r)) {  // left <= right: take the right child
+      ++child;
+      l = r;
+    }
+    Hp[pos] = l;
+    pos = child;
+    child = 2u * pos + 1u;
+  }
+  if (child == end - 1u) {
+    Hp[pos] = Hp[child];
+    pos = child;
+  }
+  hk_sift_up(Hp, pos, last);
+  return top;
+}
+
+template <int GSM>
+__device__ __forceinline__ uint8_t astar_wave_core(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag,
+                                                   uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
+                                                   int32_t* len_out) {
+  const uint32_t W = G.W;
+  const uint32_t vy = v / W, vx = v - vy * W, gy = goal / W, gx = goal - gy * W;
+  if (v == goal) {
+    *len_out = 1;
+    return NH_STAY;
+  }
+  const uint32_t tagw = tag << 22;
+  if constexpr (GSM == 2) GB[v] = 0x80u;
+  else GS[v] = tagw;
+  const uint32_t h0 = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
+  if (h0 >= (1u << 17)) {
+    *len_out = -2;
+    return NH_UNKNOWN;
+  }
+  Hp[0] = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
+  uint32_t len = 1;
+  while (len > 0) {
+    const uint64_t e = hk_pop(Hp, len);
+    const uint32_t cx = (uint32_t)(e >> 16) & 0xFFFFu, cy = (uint32_t)e & 0xFFFFu;
+    const uint32_t cg = hk(e) & 0x7FFFu;
+    const uint32_t c = cy * W + cx;
+    if (c == goal) {
+      *len_out = (int32_t)cg + 1;
+      if constexpr (GSM == 2) return (uint8_t)((GB[goal] >> 5) & 3u);
+      else return (uint8_t)((GS[goal] >> 20) & 3u);
+    }
+    const uint32_t m = G.nbmask[c];
+    uint32_t labc;
+    if constexpr (GSM == 2) labc = (GB[c] >> 5) & 3u;
+    else labc = (GS[c] >> 20) & 3u;
+    const uint32_t tg = cg + 1u;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+      if (!(m & (1u << d))) continue;
+      const uint32_t nx = d == 1 ? cx + 1 : (d == 3 ? cx - 1 : cx);
+      const uint32_t ny = d == 0 ? cy + 1 : (d == 2 ? cy - 1 : cy);
+      const uint32_t nc = ny * W + nx;
+      uint32_t oldg;
+      uint32_t man = 0;
+      if constexpr (GSM == 2) {
+        man = (nx > vx ? nx - vx : vx - nx) + (ny > vy ? ny - vy : vy - ny);
+        const uint32_t old = GB[nc];
+        oldg = (old & 0x80u) ? man + 2u * (old & 31u) : 0xFFFFFFFFu;
+      } else {
+        const uint32_t old = GS[nc];
+        oldg = ((old & 0xFFC00000u) == tagw) ? (old & GS_G_MASK) : 0xFFFFFFFFu;
+      }
+      if (tg < oldg) {
+        const uint32_t lab = cg == 0 ? d : labc;
+        const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
+        const uint32_t f = tg + h;
+        bool ovf = len >= hcap || tg >= (1u << 15) || f >= (1u << 17);
+        if constexpr (GSM == 2) {
+          const uint32_t hh = (tg - man) >> 1;
+          ovf = ovf || hh > 31u;
+          if (!ovf) GB[nc] = (uint8_t)(0x80u | (lab << 5) | hh);
+        } else {
+          if (!ovf) GS[nc] = tagw | (lab << 20) | tg;
+        }
+        if (ovf) {
+          *len_out = -2;
+          return NH_UNKNOWN;
+        }
+        hk_sift_up(Hp, len, ((uint64_t)((f << 15) | tg) << 32) | (nx << 16) | ny);
+        ++len;
+      }
+    }
+  }
+  *len_out = 2;
+  return fallback_code(G.nbmask[v], vx, vy, gx, gy);
+}
+
+// ----------------------------------------------------------------------------
 // K3 (grids of > 1024 cells): the same exact A* (astar_one), ONE QUERY PER WAVE with the heap
 // in LDS and, when the grid fits (WAVE_GS_LDS_MAX cells), the g_score words in LDS too. The
 // planner's lazy mode exits to the host whenever a step needs unresolved next hops, so K3
@@ -593,8 +715,8 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
     if (lane == 0) {
       const AstarQuery q = Q[qi];
       int32_t L = 0;
-      const uint8_t code = gs_lds == 2u ? astar_one_b8(G, q.v, q.goal, Hp, hcap, GB, &L)
-                                        : astar_one(G, q.v, q.goal, tag, Hp, hcap, GS, &L, nullptr);
+      const uint8_t code = gs_lds == 2u ? astar_wave_core<2>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L)
+                                        : astar_wave_core<1>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L);
       if (L == -2) {
         ovf[atomicAdd(novf, 1u)] = q;  // heap outgrew LDS: resolved by k_astar
       } else {
