@@ -108,6 +108,24 @@ int tsw_step(tsw_ctx *ctx, uint32_t *v, uint32_t *g, uint32_t n);
 int tsw_get_path_next(tsw_ctx *ctx, const uint32_t *start, const uint32_t *goal, uint32_t k,
                       uint32_t *next, int32_t *len);
 
+/* Batched decentralized decision: compute_next_move_with_tswap
+ * (src/bin/decentralized/agent.rs:329-462) for n agents, each with its own local view.
+ * Agent i: cell my_v[i], goal my_g[i] (free cells, else TSW_EINVAL — the reference panics at
+ * pos2id[&my_pos], :358); its nearby list is entries nb_off[i] .. nb_off[i+1]-1 of nb_v/nb_g
+ * (the other agents' cell / goal cell ids in NearbyAgents::get_nearby order, self excluded,
+ * :108-153; an id >= w*h or a blocked cell means "not on the map", :389-393).
+ * Outputs per agent: act[i] = TSW_ACT_* (TswapAction, :321-326); cell[i] = Move destination
+ * (the agent's own cell for Rule 1); partner[i] = list index of the goal-swap partner
+ * (0xFFFFFFFF otherwise); npart[i] = number of rotation participants, whose list indices are
+ * part[nb_off[i] + i .. + npart[i]) (part holds nb_off[n] + n entries). */
+#define TSW_ACT_MOVE 0u
+#define TSW_ACT_GOAL_SWAP 1u
+#define TSW_ACT_ROTATION 2u
+#define TSW_ACT_WAIT 3u
+int tsw_decide(tsw_ctx *ctx, const uint32_t *my_v, const uint32_t *my_g, uint32_t n, const uint32_t *nb_off,
+               const uint32_t *nb_v, const uint32_t *nb_g, uint32_t *act, uint32_t *cell, uint32_t *partner,
+               uint32_t *npart, uint32_t *part);
+
 /* K1: BFS distance tables for k goal cells, u16 per cell, row-major
  * (TSW_DIST_INF for blocked/unreachable). out: host buffer k*w*h. */
 int tsw_dist_tables(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint16_t *out);

@@ -45,6 +45,9 @@ def lib():
         L.orc_tswap_step.argtypes = [ctypes.c_void_p, P(u32), P(u32), u32]
         L.orc_tswap_mapd.argtypes = [ctypes.c_void_p, P(u32), u32, P(u32), u32, u32, P(u64), P(u32)]
         L.orc_tswap_mapd.restype = i32
+        L.orc_decide.argtypes = [ctypes.c_void_p, u32, u32, P(u32), P(u32), u32, P(u32), P(u32), P(u32), P(u32),
+                                 P(u32)]
+        L.orc_decide.restype = ctypes.c_int
         L.orc_stat_calls.argtypes = [ctypes.c_void_p]
         L.orc_stat_calls.restype = u64
         L.orc_stat_pops.argtypes = [ctypes.c_void_p]
@@ -109,6 +112,20 @@ class OracleGraph:
         if T < 0:
             raise ValueError("invalid input (reference would panic)")
         return out[:n, :T], (gout[:n, :T] if gout is not None else None)
+
+    def decide(self, my_v: int, my_g: int, nb_v, nb_g):
+        """compute_next_move_with_tswap (agent.rs:329-462) for one agent. Returns
+        (act, cell, partner, participants) with act 0 Move, 1 WaitForGoalSwap, 2 WaitForRotation,
+        3 Wait; partner / participants are indices into the nearby list."""
+        nv = np.ascontiguousarray(nb_v, dtype=np.uint32)
+        ng = np.ascontiguousarray(nb_g, dtype=np.uint32)
+        act, cell, partner, npart = (ctypes.c_uint32(0) for _ in range(4))
+        part = np.zeros(nv.size + 1, dtype=np.uint32)
+        rc = lib().orc_decide(self.ptr, my_v, my_g, _u32p(nv), _u32p(ng), nv.size, ctypes.byref(act),
+                              ctypes.byref(cell), ctypes.byref(partner), ctypes.byref(npart), _u32p(part))
+        if rc != 0:
+            raise ValueError("agent cell not free (reference panics)")
+        return act.value, cell.value, partner.value, [int(x) for x in part[:npart.value]]
 
     def calls(self):
         return lib().orc_stat_calls(self.ptr)

@@ -271,3 +271,57 @@ def tswap_mapd(grid, initial_positions, tasks, max_t=2000, trace_goals=None):
         if (all(used) and all(s == "idle" for s in st)) or t > max_t:
             break
     return paths
+
+
+def compute_next_move_with_tswap(my_pos, my_goal, nearby, graph: Graph):
+    """src/bin/decentralized/agent.rs:329-462, with POSITIONS (x, y). nearby: list of
+    (current_pos, goal_pos) in get_nearby order (self excluded). Returns (kind, payload):
+    ("move", pos) | ("swap", list index) | ("rotation", [list indices]) | ("wait", None)."""
+    def find(pos):  # nearby_agents.iter().find(|a| a.current_pos == pos)
+        for k, a in enumerate(nearby):
+            if a[0] == pos:
+                return k
+        return None
+
+    if my_pos == my_goal:  # Rule 1
+        return ("move", my_pos)
+    path = graph.get_path(graph.pos2id[my_pos], graph.pos2id[my_goal])
+    if len(path) < 2:
+        return ("move", my_pos)
+    next_pos = graph.id2pos[path[1]]
+    b = find(next_pos)
+    if b is None:  # Rule 2
+        return ("move", next_pos)
+    if nearby[b][0] == nearby[b][1]:  # Rule 3
+        return ("swap", b)
+    a_p = [my_pos]  # Rule 4
+    cur = b
+    found = False
+    while True:
+        cpos, cgoal = nearby[cur]
+        if cpos == cgoal:
+            break
+        if cpos not in graph.pos2id or cgoal not in graph.pos2id:
+            break
+        ap = graph.get_path(graph.pos2id[cpos], graph.pos2id[cgoal])
+        if len(ap) < 2:
+            break
+        nd = graph.id2pos[ap[1]]
+        nx = find(nd)
+        if nx is None:
+            break
+        if nearby[nx][0] in a_p:
+            if nearby[nx][0] == my_pos:
+                found = True
+            else:
+                a_p.clear()
+            break
+        a_p.append(cpos)
+        cur = nx
+    if found and len(a_p) > 1:
+        parts = [find(p) for p in a_p]
+        parts = [k for k in parts if k is not None]
+        if len(parts) > 1:
+            return ("rotation", parts)
+        return ("wait", None)
+    return ("wait", None)

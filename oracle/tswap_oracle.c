@@ -460,3 +460,83 @@ out:
     free(dlv);
     return T;
 }
+
+/* ---- decentralized decision --------------------------------------
+ * compute_next_move_with_tswap, src/bin/decentralized/agent.rs:329-462, for one agent.
+ * The local view is the caller's nearby list (agent.rs:108-153: every other agent within
+ * Manhattan radius, self excluded) in the caller's order — `find` takes the FIRST entry at a
+ * position (:369, :399-401, :435). Positions are cell ids; a position that is not a free cell
+ * is "not in pos2id" (:392-393 break). */
+static inline int64_t first_at(const uint32_t *nv, uint32_t nn, uint32_t pos) {
+    for (uint32_t k = 0; k < nn; k++)
+        if (nv[k] == pos) return k;
+    return -1;
+}
+
+int orc_decide(orc_graph *gr, uint32_t my_v, uint32_t my_g, const uint32_t *nb_v, const uint32_t *nb_g,
+               uint32_t nn, uint32_t *act, uint32_t *cell, uint32_t *partner, uint32_t *npart, uint32_t *part) {
+    if (my_v >= gr->ncell || my_g >= gr->ncell || !gr->free_[my_v] || !gr->free_[my_g]) return -1; /* :358 panics */
+    *cell = my_v;
+    *partner = UINT32_MAX;
+    *npart = 0;
+    if (my_v == my_g) { /* Rule 1 :355-356 */
+        *act = ORC_ACT_MOVE;
+        return 0;
+    }
+    uint32_t next;
+    int32_t len = orc_get_path_next(gr, my_v, my_g, &next, NULL); /* :358 */
+    if (len < 2) { /* :359-360 */
+        *act = ORC_ACT_MOVE;
+        return 0;
+    }
+    int64_t b = first_at(nb_v, nn, next); /* :369 */
+    if (b < 0) { /* Rule 2 :454-456 */
+        *act = ORC_ACT_MOVE;
+        *cell = next;
+        return 0;
+    }
+    if (nb_v[b] == nb_g[b]) { /* Rule 3 :371-377 */
+        *act = ORC_ACT_GOAL_SWAP;
+        *partner = (uint32_t)b;
+        return 0;
+    }
+    /* Rule 4 :379-427 — a_p holds POSITIONS */
+    uint32_t *a_p = (uint32_t *)malloc(sizeof(uint32_t) * (nn + 2));
+    size_t ap_len = 0;
+    a_p[ap_len++] = my_v;
+    uint32_t cur = (uint32_t)b;
+    int found = 0;
+    for (;;) {
+        if (nb_v[cur] == nb_g[cur]) break; /* :383-385 */
+        const uint32_t cv = nb_v[cur], cg = nb_g[cur];
+        if (cv >= gr->ncell || !gr->free_[cv] || cg >= gr->ncell || !gr->free_[cg]) break; /* :389-393 */
+        uint32_t nd;
+        if (orc_get_path_next(gr, cv, cg, &nd, NULL) < 2) break; /* :393-397 */
+        int64_t nx = first_at(nb_v, nn, nd); /* :399-401 */
+        if (nx < 0) break; /* :416-419 */
+        int in_ap = 0;
+        for (size_t k = 0; k < ap_len; k++)
+            if (a_p[k] == nb_v[nx]) in_ap = 1;
+        if (in_ap) { /* :403-411 */
+            if (nb_v[nx] == my_v) found = 1;
+            else ap_len = 0;
+            break;
+        }
+        a_p[ap_len++] = cv; /* :413 */
+        cur = (uint32_t)nx;
+    }
+    if (found && ap_len > 1) { /* :430-447 */
+        uint32_t np = 0;
+        for (size_t k = 0; k < ap_len; k++) {
+            int64_t a = first_at(nb_v, nn, a_p[k]);
+            if (a >= 0) part[np++] = (uint32_t)a;
+        }
+        *npart = np;
+        *act = np > 1 ? ORC_ACT_ROTATION : ORC_ACT_WAIT;
+        if (np <= 1) *npart = 0;
+    } else { /* Rule 5 :449-451 */
+        *act = ORC_ACT_WAIT;
+    }
+    free(a_p);
+    return 0;
+}

@@ -66,6 +66,19 @@ int32_t orc_tswap_mapd(orc_graph *gr, const uint32_t *starts_xy, uint32_t n,
                        const uint32_t *tasks_xyxy, uint32_t m, uint32_t max_t,
                        uint64_t *rec_out, uint32_t *goal_out);
 
+/* Decentralized per-agent decision, compute_next_move_with_tswap
+ * (src/bin/decentralized/agent.rs:329-462). nb_v/nb_g: the nearby agents' current/goal cells
+ * in the caller's list order (self excluded, agent.rs:134). Outputs: act (ORC_ACT_*), cell
+ * (Move destination), partner (list index, GOAL_SWAP), npart + part[0..npart) (list indices
+ * of the rotation participants, ROTATION; part must hold nn + 1 entries).
+ * Returns -1 if my_v or my_g is not a free cell (the reference panics, agent.rs:358). */
+#define ORC_ACT_MOVE 0u
+#define ORC_ACT_GOAL_SWAP 1u
+#define ORC_ACT_ROTATION 2u
+#define ORC_ACT_WAIT 3u
+int orc_decide(orc_graph *gr, uint32_t my_v, uint32_t my_g, const uint32_t *nb_v, const uint32_t *nb_g,
+               uint32_t nn, uint32_t *act, uint32_t *cell, uint32_t *partner, uint32_t *npart, uint32_t *part);
+
 /* Counter of get_path calls / heap pops since the graph was created. */
 uint64_t orc_stat_calls(orc_graph *gr);
 uint64_t orc_stat_pops(orc_graph *gr);

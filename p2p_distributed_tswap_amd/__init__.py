@@ -33,6 +33,8 @@ LIB_PATH = os.path.join(_HERE, "libtswap_hip.so")
 
 TSW_OK, TSW_EINVAL, TSW_ENOMEM, TSW_EHIP, TSW_EOVERFLOW = 0, -22, -12, -5, -75
 TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP = 1, 2
+# TswapAction (bin/decentralized/agent.rs:321-326), include/tswap.h TSW_ACT_*
+TSW_ACT_MOVE, TSW_ACT_GOAL_SWAP, TSW_ACT_ROTATION, TSW_ACT_WAIT = 0, 1, 2, 3
 DIST_INF = 0xFFFF
 
 
@@ -98,7 +100,7 @@ class Stats(ctypes.Structure):
 # every symbol declared in include/tswap.h (tests check the .so exports them)
 EXPORTED_SYMBOLS = (
     "tsw_create", "tsw_destroy", "tsw_last_error", "tsw_plan_mapd", "tsw_plan_mapd_trace",
-    "tsw_step", "tsw_get_path_next", "tsw_dist_tables", "tsw_dist_tables_device",
+    "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables", "tsw_dist_tables_device",
     "tsw_import_tables_device", "tsw_next_hop_tables", "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing",
 )
 
@@ -126,6 +128,8 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_plan_mapd_trace.argtypes = [vp, P(_Point), u32, P(_Task), u32, u32, P(_Rec), P(u32), P(u32)]
     lib.tsw_step.argtypes = [vp, P(u32), P(u32), u32]
     lib.tsw_get_path_next.argtypes = [vp, P(u32), P(u32), u32, P(u32), P(i32)]
+    lib.tsw_decide.argtypes = [vp, P(u32), P(u32), u32, P(u32), P(u32), P(u32), P(u32), P(u32), P(u32), P(u32),
+                               P(u32)]
     lib.tsw_dist_tables.argtypes = [vp, P(u32), u32, P(ctypes.c_uint16)]
     lib.tsw_dist_tables_device.argtypes = [vp, P(u32), u32, vp]
     lib.tsw_import_tables_device.argtypes = [vp, P(u32), u32, vp]
@@ -134,7 +138,7 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_get_stats.argtypes = [vp, P(Stats)]
     lib.tsw_reset_stats.argtypes = [vp]
     lib.tsw_set_timing.argtypes = [vp, ctypes.c_int]
-    for name in ("tsw_plan_mapd", "tsw_plan_mapd_trace", "tsw_step", "tsw_get_path_next", "tsw_dist_tables",
+    for name in ("tsw_plan_mapd", "tsw_plan_mapd_trace", "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables",
                  "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_clear_tables", "tsw_next_hop_tables", "tsw_get_stats", "tsw_reset_stats",
                  "tsw_set_timing"):
         getattr(lib, name).restype = ctypes.c_int
@@ -247,6 +251,36 @@ class Planner:
             raise TswapError(TSW_EINVAL, "v and g must have the same length")
         self._check(self._lib.tsw_step(self._ctx, _u32p(v), _u32p(g), v.size))
         return v, g
+
+    # --- decentralized decision (bin/decentralized/agent.rs:329-462) ----------
+    def decide(self, my_v, my_g, nearby):
+        """Batched compute_next_move_with_tswap. my_v, my_g: (n,) cell ids; nearby: list of n
+        sequences of (cell, goal_cell) pairs (the agent's get_nearby list, self excluded, in
+        order). Returns a list of (act, cell, partner, participants) with act one of
+        TSW_ACT_MOVE / _GOAL_SWAP / _ROTATION / _WAIT and list indices for partner/participants."""
+        my_v = np.ascontiguousarray(my_v, dtype=np.uint32)
+        my_g = np.ascontiguousarray(my_g, dtype=np.uint32)
+        n = my_v.size
+        if my_g.size != n or len(nearby) != n:
+            raise TswapError(TSW_EINVAL, "my_v, my_g and nearby must have the same length")
+        off = np.zeros(n + 1, dtype=np.uint32)
+        off[1:] = np.cumsum([len(x) for x in nearby]) if n else []
+        flat = [p for x in nearby for p in x]
+        nv = np.array([p[0] for p in flat], dtype=np.uint32)
+        ng = np.array([p[1] for p in flat], dtype=np.uint32)
+        act = np.zeros(n, dtype=np.uint32)
+        cell = np.zeros(n, dtype=np.uint32)
+        partner = np.zeros(n, dtype=np.uint32)
+        npart = np.zeros(n, dtype=np.uint32)
+        part = np.zeros(int(off[-1]) + n + 1, dtype=np.uint32)
+        self._check(self._lib.tsw_decide(self._ctx, _u32p(my_v), _u32p(my_g), n, _u32p(off), _u32p(nv),
+                                         _u32p(ng), _u32p(act), _u32p(cell), _u32p(partner), _u32p(npart),
+                                         _u32p(part)))
+        out = []
+        for i in range(n):
+            b = int(off[i]) + i
+            out.append((int(act[i]), int(cell[i]), int(partner[i]), [int(x) for x in part[b:b + npart[i]]]))
+        return out
 
     # --- get_path -----------------------------------------------------------
     def get_path_next(self, start: np.ndarray, goal: np.ndarray):

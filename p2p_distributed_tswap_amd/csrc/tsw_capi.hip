@@ -1026,6 +1026,129 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   return TSW_OK;
 }
 
+int tsw_decide(tsw_ctx* c, const uint32_t* my_v, const uint32_t* my_g, uint32_t n, const uint32_t* nb_off,
+               const uint32_t* nb_v, const uint32_t* nb_g, uint32_t* act, uint32_t* cell, uint32_t* partner,
+               uint32_t* npart, uint32_t* part) {
+  if (!c) return TSW_EINVAL;
+  if (n == 0) return TSW_OK;
+  if (!my_v || !my_g || !nb_off || !act || !cell || !partner || !npart || !part) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  const uint32_t tot = nb_off[n];
+  if (nb_off[0] != 0) RET(TSW_EINVAL, "nb_off[0] must be 0");
+  for (uint32_t i = 0; i < n; ++i)
+    if (nb_off[i + 1] < nb_off[i]) RET(TSW_EINVAL, "nb_off must be non-decreasing");
+  if (tot && (!nb_v || !nb_g)) RET(TSW_EINVAL, "null nearby list");
+  // goal tables for every goal a decision can route to: own goals and the nearby agents'
+  // (those on free cells — a goal off the map stops the chase, agent.rs:389-393)
+  std::vector<uint32_t> goals;
+  goals.reserve(n + tot);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!cell_id_ok(c, my_v[i]) || !cell_id_ok(c, my_g[i]))
+      RET(TSW_EINVAL, "agent cell or goal off-grid or blocked (reference panics at agent.rs:358)");
+    goals.push_back(my_g[i]);
+  }
+  for (uint32_t k = 0; k < tot; ++k)
+    if (cell_id_ok(c, nb_g[k]) && cell_id_ok(c, nb_v[k])) goals.push_back(nb_g[k]);
+  TRY(ensure_tables(c, goals));
+  // device copies: inputs, outputs, pending lists (ping-pong)
+  const size_t nb = std::max<uint32_t>(tot, 1u);
+  std::vector<uint32_t> idx(n);
+  for (uint32_t i = 0; i < n; ++i) idx[i] = i;
+  uint32_t* d = nullptr;
+  const size_t words = 2 * (size_t)n + (n + 1) + 2 * nb + 4 * (size_t)n + (tot + n) + 2 * (size_t)n + 2;
+  HIPCHK(hipMalloc(&d, words * 4));
+  uint32_t *d_v = d, *d_g = d_v + n, *d_off = d_g + n, *d_nv = d_off + n + 1, *d_ng = d_nv + nb;
+  uint32_t *d_act = d_ng + nb, *d_cell = d_act + n, *d_par = d_cell + n, *d_np = d_par + n;
+  uint32_t *d_part = d_np + n, *d_q0 = d_part + tot + n, *d_q1 = d_q0 + n, *d_cnt = d_q1 + n;
+  auto cleanup = [&]() { hipFree(d); };
+  auto fail = [&](hipError_t e) {
+    cleanup();
+    c->err = std::string("HIP: ") + hipGetErrorString(e);
+    return TSW_EHIP;
+  };
+  hipError_t e;
+#define DCHK(x)                                 \
+  do {                                          \
+    if ((e = (x)) != hipSuccess) return fail(e); \
+  } while (0)
+  DCHK(hipMemcpyAsync(d_v, my_v, n * 4ull, hipMemcpyHostToDevice, c->s));
+  DCHK(hipMemcpyAsync(d_g, my_g, n * 4ull, hipMemcpyHostToDevice, c->s));
+  DCHK(hipMemcpyAsync(d_off, nb_off, (n + 1) * 4ull, hipMemcpyHostToDevice, c->s));
+  if (tot) {
+    DCHK(hipMemcpyAsync(d_nv, nb_v, tot * 4ull, hipMemcpyHostToDevice, c->s));
+    DCHK(hipMemcpyAsync(d_ng, nb_g, tot * 4ull, hipMemcpyHostToDevice, c->s));
+  }
+  DCHK(hipMemcpyAsync(d_q0, idx.data(), n * 4ull, hipMemcpyHostToDevice, c->s));
+  if (int r = ensure_queue(c, std::max<size_t>(2 * ((size_t)n + tot), 1024)); r != TSW_OK) {
+    cleanup();
+    return r;
+  }
+  DecideArgs A{};
+  A.W = c->G.W;
+  A.ncell = c->G.ncell;
+  A.my_v = d_v;
+  A.my_g = d_g;
+  A.nb_off = d_off;
+  A.nb_v = d_nv;
+  A.nb_g = d_ng;
+  A.nbmask = c->d_nbmask;
+  A.goal_tab = c->d_goal_tab;
+  A.nh = c->d_nh;
+  A.nstride = c->tstride;
+  A.act = d_act;
+  A.cell = d_cell;
+  A.partner = d_par;
+  A.npart = d_np;
+  A.part = d_part;
+  A.Q = c->d_Q;
+  A.qcap = (uint32_t)c->qcap;
+  A.err = &c->d_stat->err;
+  uint32_t nq = n;
+  uint32_t* qin = d_q0;
+  uint32_t* qout = d_q1;
+  for (int round = 0; nq > 0; ++round) {
+    if (round > 1 + 2 * (int)std::min<uint64_t>(tot + n, 1u << 20)) {
+      cleanup();
+      RET(TSW_EINVAL, "decision made no progress");
+    }
+    A.qidx = qin;
+    A.nq = nq;
+    A.pending_out = qout;
+    A.qcount = d_cnt;
+    A.npending = d_cnt + 1;
+    DCHK(hipMemsetAsync(d_cnt, 0, 8, c->s));
+    DCHK(launch_decide(A, c->s));
+    uint32_t h[2] = {0, 0};
+    DCHK(hipMemcpyAsync(h, d_cnt, 8, hipMemcpyDeviceToHost, c->s));
+    DCHK(hipStreamSynchronize(c->s));
+    if (int r = check_err(c); r != TSW_OK) {
+      cleanup();
+      return r;
+    }
+    if (h[1] == 0) break;
+    if (h[0] == 0 || h[0] > c->qcap) {
+      cleanup();
+      RET(TSW_EINVAL, "decision stalled on an unresolvable next hop");
+    }
+    if (int r = run_astar(c, c->d_Q, h[0], true, nullptr, nullptr); r != TSW_OK) {
+      cleanup();
+      return r;
+    }
+    nq = h[1];
+    std::swap(qin, qout);
+  }
+  DCHK(hipMemcpyAsync(act, d_act, n * 4ull, hipMemcpyDeviceToHost, c->s));
+  DCHK(hipMemcpyAsync(cell, d_cell, n * 4ull, hipMemcpyDeviceToHost, c->s));
+  DCHK(hipMemcpyAsync(partner, d_par, n * 4ull, hipMemcpyDeviceToHost, c->s));
+  DCHK(hipMemcpyAsync(npart, d_np, n * 4ull, hipMemcpyDeviceToHost, c->s));
+  DCHK(hipMemcpyAsync(part, d_part, ((size_t)tot + n) * 4ull, hipMemcpyDeviceToHost, c->s));
+  DCHK(hipStreamSynchronize(c->s));
+#undef DCHK
+  cleanup();
+  resolve_timing(c);
+  return TSW_OK;
+}
+
 int tsw_get_path_next(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, uint32_t k, uint32_t* next,
                       int32_t* len) {
   if (!c) return TSW_EINVAL;

@@ -65,5 +65,6 @@ constexpr uint32_t ERR_G_OVERFLOW = 4u;
 constexpr uint32_t ERR_NO_TABLE = 8u;
 constexpr uint32_t ERR_WALK_OVERFLOW = 16u;
 constexpr uint32_t ERR_BFS_LIST = 32u;     // k_bfs_wave: a queued word gained no cell (logic error)
+constexpr uint32_t ERR_DECIDE_LIST = 64u;  // k_decide: a nearby list longer than DEC_MAX_LIST
 
 }  // namespace tsw

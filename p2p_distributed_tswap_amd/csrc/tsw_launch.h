@@ -84,6 +84,32 @@ hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq,
                              uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
                              AstarQuery* ovf, uint32_t* novf, uint32_t hcap /*0: default*/, hipStream_t s);
 
+// Batched decentralized decision (tsw_decide.hip, agent.rs:329-462).
+constexpr uint32_t DEC_ACT_MOVE = 0, DEC_ACT_GOAL_SWAP = 1, DEC_ACT_ROTATION = 2, DEC_ACT_WAIT = 3;
+struct DecideArgs {
+  uint32_t W, ncell;
+  const uint32_t* my_v;    // [n] agent cells
+  const uint32_t* my_g;    // [n] goal cells
+  const uint32_t* nb_off;  // [n + 1] nearby-list offsets
+  const uint32_t* nb_v;    // nearby agents' cells (any value >= ncell: off the map)
+  const uint32_t* nb_g;    // nearby agents' goal cells
+  const uint8_t* nbmask;
+  const int32_t* goal_tab;
+  uint8_t* nh;
+  uint64_t nstride;
+  const uint32_t* qidx;    // agents to decide in this launch
+  uint32_t nq;
+  uint32_t *act, *cell, *partner, *npart;
+  uint32_t* part;          // per agent i: nb_off[i] + i .. + nn_i + 1 (participant list indices)
+  AstarQuery* Q;
+  uint32_t* qcount;
+  uint32_t qcap;
+  uint32_t* pending_out;   // agents parked on an unresolved next hop
+  uint32_t* npending;
+  uint32_t* err;
+};
+hipError_t launch_decide(const DecideArgs& A, hipStream_t s);
+
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
                                   uint32_t qcap, hipStream_t s);

@@ -165,7 +165,46 @@ def rows_to_array(rows) -> np.ndarray:
     return np.frombuffer("".join(rows).encode("latin-1"), dtype=np.uint8).reshape(len(rows), len(rows[0])).copy()
 
 
-# ---- MovingAI .map I/O --------------------------------
+# ---- map text / MovingAI I/O --------------------------
+def parse_map(text: str) -> list:
+    """The reference's parse_map (src/bin/centralized/manager.rs:25-34): every '\\r' removed,
+    lines split, lines that are blank after trimming dropped, each kept line's characters as a
+    row (no other trimming). Rows must come out equally long for the C ABI (the reference
+    indexes grid[y][x] for x < grid[0].len(), tswap.rs:51-56, and panics on a short row)."""
+    rows = [ln for ln in text.replace("\r", "").splitlines() if ln.strip()]
+    if rows and any(len(r) != len(rows[0]) for r in rows):
+        raise ValueError("ragged map: every row must be as long as the first (tswap.rs:51-56)")
+    return rows
+
+
+def read_scen(path: str):
+    """MovingAI .scen (\"version 1\" header; per line: bucket map width height sx sy gx gy
+    optimal). Returns (starts (n,2) uint32, goals (n,2) uint32, optimal (n,) float64) as
+    (x, y) points — the Point convention of src/map/map.rs:4 (x = column, y = row)."""
+    st, gl, opt = [], [], []
+    with open(path) as f:
+        for ln in f:
+            parts = ln.split()
+            if len(parts) < 9 or parts[0].lower() == "version":
+                continue
+            sx, sy, gx, gy = (int(v) for v in parts[4:8])
+            st.append((sx, sy))
+            gl.append((gx, gy))
+            opt.append(float(parts[8]))
+    return (np.array(st, dtype=np.uint32).reshape(-1, 2), np.array(gl, dtype=np.uint32).reshape(-1, 2),
+            np.array(opt, dtype=np.float64))
+
+
+def write_scen(path: str, map_name: str, rows, starts, goals, optimal=None) -> None:
+    h, w = len(rows), len(rows[0])
+    with open(path, "w") as f:
+        f.write("version 1\n")
+        for i, ((sx, sy), (gx, gy)) in enumerate(zip(starts, goals)):
+            o = float(optimal[i]) if optimal is not None else 0.0
+            f.write(f"0\t{map_name}\t{w}\t{h}\t{sx}\t{sy}\t{gx}\t{gy}\t{o:.8f}\n")
+
+
+# ---- MovingAI .map files ------------------------------------------------------
 def write_movingai(path: str, rows) -> None:
     with open(path, "w") as f:
         f.write("type octile\n")

@@ -77,3 +77,26 @@ def test_movingai_roundtrip(tmp_path):
     p = tmp_path / "m.map"
     maps.write_movingai(str(p), rows)
     assert maps.read_movingai(str(p)) == rows
+
+
+def test_parse_map_mirrors_reference():
+    """parse_map (centralized/manager.rs:25-34): '\\r' removed, blank lines dropped, rows kept
+    verbatim; the bundled MAP literal starts with a newline (src/map/map.rs:5)."""
+    text = "\n" + "\r\n".join(["." * 5, "..@..", "   ", "@...."]) + "\r\n\n"
+    assert maps.parse_map(text) == [".....", "..@..", "@...."]
+    assert maps.parse_map("\n" + "\n".join(["." * 100] * 100) + "\n") == maps.bundled_map()
+    with pytest.raises(ValueError):
+        maps.parse_map("...\n..\n")
+
+
+def test_scen_round_trip(tmp_path):
+    rows = maps.random_map(20, 12, 0.2, 4)
+    st = np.array([[1, 2], [3, 4]], dtype=np.uint32)
+    gl = np.array([[5, 6], [7, 8]], dtype=np.uint32)
+    p = tmp_path / "x.scen"
+    maps.write_scen(str(p), "x.map", rows, st, gl, [3.0, 4.5])
+    s2, g2, o2 = maps.read_scen(str(p))
+    assert np.array_equal(s2, st) and np.array_equal(g2, gl) and list(o2) == [3.0, 4.5]
+    m = tmp_path / "x.map"
+    maps.write_movingai(str(m), rows)
+    assert maps.read_movingai(str(m)) == rows
