@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--bfs-goals", type=int, default=10000)
     ap.add_argument("--bfs-reps", type=int, default=3)
     ap.add_argument("--config", default="c2_random_32_32_20")
+    ap.add_argument("--nexthop", choices=("auto", "eager", "lazy"), default="auto",
+                    help="next-hop resolution policy (TSW_F_EAGER_NEXTHOP / TSW_F_LAZY_NEXTHOP)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, default) or gloo (rehearsing N ranks on one GPU)")
     return ap.parse_args()
@@ -118,7 +120,10 @@ def main():
     rows = fac()
     h, w = len(rows), len(rows[0])
     starts, tasks = maps.make_instance(rows, n_agents, n_tasks, seed + rank)
-    planner = Planner(rows, device=dev)
+    from p2p_distributed_tswap_amd import TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP
+
+    pflags = {"auto": 0, "eager": TSW_F_EAGER_NEXTHOP, "lazy": TSW_F_LAZY_NEXTHOP}[args.nexthop]
+    planner = Planner(rows, device=dev, flags=pflags)
 
     def one_plan():
         planner.clear_tables()
@@ -172,6 +177,10 @@ def main():
         "traffic_source": traffic_src,
         "avg_launch_us": round(avg_launch_ms * 1e3, 3),
         "launches": int(dom_launches),
+        "note": ("k_plan is one persistent workgroup executing tswap_step's sequential agent-order "
+                 "semantics (tswap.rs:180-285) as exact parallel rounds; it is latency/barrier-bound, "
+                 "so its HBM fraction is tiny by construction. K1 (bfs.roofline) is the HBM-bound kernel."
+                 if dom.startswith("k_plan") else None),
         "algorithmic_bytes_per_launch": round(per_launch_bytes, 1),
         "device_ms_by_kernel": {k.split()[0]: round(v[0], 3) for k, v in cats.items()},
     }

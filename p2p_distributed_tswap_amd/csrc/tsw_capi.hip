@@ -641,7 +641,8 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.occ = c->d_occ;
   P.mu = c->d_mu;
   P.has_dups = *c->h_dups;
-  P.prefetch = getenv("TSW_NO_PREFETCH") ? 0u : 1u;
+  // speculative next-hop prefetch only pays in lazy mode (eager tables have nothing unresolved)
+  P.prefetch = (getenv("TSW_NO_PREFETCH") || eager_policy(c, 0)) ? 0u : 1u;
   P.pick_xy = c->d_pick_xy;
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;
@@ -681,7 +682,8 @@ int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
   const size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds);
   // one lane per agent in the parallel passes when possible; >= 4 waves for the task argmin
-  const uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
+  uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
+  if (const char* e = getenv("TSW_PLAN_BLOCK")) block = (uint32_t)std::max(64, std::min(atoi(e), 1024)) / 64u * 64u;
   for (uint64_t round = 0;; ++round) {
     if (round > 16ull * P.n + 4096ull * (init.max_t + 1)) RET(TSW_EINVAL, "plan kernel made no progress");
     {
@@ -700,6 +702,9 @@ int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     if (k.status == PLAN_DONE) {
       c->chase_id = k.chase_id;
       c->st.rule_rounds += k.rule_rounds;
+      if (getenv("TSW_PLAN_DEBUG"))
+        fprintf(stderr, "[k_plan] steps %u rule rounds %u move rounds %u launches %llu\n", k.steps_run,
+                k.rule_rounds, k.move_rounds, (unsigned long long)round + 1ull);
       // pairs the rules prefetch queued but no firing needed: resolve them so no table entry
       // is left PENDING for later calls
       if (k.qcount > 0) {

@@ -37,7 +37,7 @@ struct PlanCtl {
   uint32_t miss;      // serial movement scan: 1 = unresolved next hop, 2 = goal without table
   uint32_t steps_run;
   uint32_t rule_rounds;  // first-firing rounds executed (rules phase)
-  uint32_t pad1;
+  uint32_t move_rounds;  // decidability rounds executed (movement phase)
 };
 
 struct PlanArgs {

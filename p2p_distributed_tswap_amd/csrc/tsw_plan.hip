@@ -570,12 +570,15 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
               }
             } else {  // rule 4: rotate targets along the cycle b -> s -> ... -> last -> b
               uint32_t L = 0;
-              for (uint32_t a = b; L == 0 || a != b; a = S.SUCC[a]) P.ap[L++] = a;
-              const uint32_t last = P.ap[L - 1];
+              // cycle members in S.F2 (free until the rules_init this rotation triggers; LDS when
+              // the agent arrays are): the walk below re-reads them serially
+              uint32_t* ap = S.F2;
+              for (uint32_t a = b; L == 0 || a != b; a = S.SUCC[a]) ap[L++] = a;
+              const uint32_t last = ap[L - 1];
               const uint32_t last_goal = S.G[last];
               const int32_t last_tab = S.GT[last];
               for (uint32_t kk = L - 1; kk >= 1; --kk) {
-                const uint32_t a = P.ap[kk], pa = P.ap[kk - 1];
+                const uint32_t a = ap[kk], pa = ap[kk - 1];
                 S.G[a] = S.G[pa];
                 S.GT[a] = S.GT[pa];
                 S.NHC[a] = NHC_DIRTY;
@@ -643,7 +646,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (tid == 0) s_ctl.i = 1;  // DEC initialised for this step (survives relaunches)
       }
       for (;;) {
-        if (tid == 0) s_miss = 0;
+        if (tid == 0) {
+          s_miss = 0;
+          s_ctl.move_rounds += 1;
+        }
         __syncthreads();
         // A: target cell of every open agent; reset MU at its target and its own cell
         int open = 0;
