@@ -656,6 +656,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.grec = want_goals ? c->d_grec : nullptr;
   P.ctl = c->d_ctl;
   P.sec_ticks = c->d_ticks;
+  P.dbg = getenv("TSW_PLAN_DEBUG") ? 1u : 0u;
   // LDS residency, in priority order: agents, occupancy grid, task table
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
@@ -702,9 +703,14 @@ int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     if (k.status == PLAN_DONE) {
       c->chase_id = k.chase_id;
       c->st.rule_rounds += k.rule_rounds;
-      if (getenv("TSW_PLAN_DEBUG"))
-        fprintf(stderr, "[k_plan] steps %u rule rounds %u move rounds %u launches %llu\n", k.steps_run,
-                k.rule_rounds, k.move_rounds, (unsigned long long)round + 1ull);
+      if (getenv("TSW_PLAN_DEBUG")) {
+        unsigned long long tk[16];
+        HIPCHK(hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[k_plan] steps %u rule rounds %u move rounds %u launches %llu | move A-E us %.0f %.0f %.0f %.0f %.0f"
+                " | rules scan %.0f fire %.0f relabel %.0f\n", k.steps_run, k.rule_rounds, k.move_rounds,
+                (unsigned long long)round + 1ull, tk[8] / 100.0, tk[9] / 100.0, tk[10] / 100.0, tk[11] / 100.0,
+                tk[12] / 100.0, tk[13] / 100.0, tk[14] / 100.0, tk[15] / 100.0);
+      }
       // pairs the rules prefetch queued but no firing needed: resolve them so no table entry
       // is left PENDING for later calls
       if (k.qcount > 0) {
@@ -946,8 +952,8 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned status", e);
   if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
-  if ((e = hipMalloc(&c->d_ticks, 8 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
-  if ((e = hipMemsetAsync(c->d_ticks, 0, 8 * sizeof(unsigned long long), c->s)) != hipSuccess)
+  if ((e = hipMalloc(&c->d_ticks, 16 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
+  if ((e = hipMemsetAsync(c->d_ticks, 0, 16 * sizeof(unsigned long long), c->s)) != hipSuccess)
     return fail("memset ticks", e);
   hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, c->device);
   if (c->wall_khz <= 0) c->wall_khz = 100000;
@@ -1353,7 +1359,7 @@ int tsw_reset_stats(tsw_ctx* c) {
   const uint64_t tabs = c->st.tables;
   c->st = tsw_stats{};
   c->st.tables = tabs;
-  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 8 * sizeof(unsigned long long), c->s);
+  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 16 * sizeof(unsigned long long), c->s);
   return TSW_OK;
 }
 

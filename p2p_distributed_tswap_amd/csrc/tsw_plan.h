@@ -71,7 +71,8 @@ struct PlanArgs {
   uint64_t* rec;
   uint32_t* grec;
   PlanCtl* ctl;
-  unsigned long long* sec_ticks;  // [8] wall-clock ticks spent per section (diagnostics)
+  unsigned long long* sec_ticks;  // [16] wall-clock ticks per section [0..7] and sub-phase [8..15] (diagnostics)
+  uint32_t dbg;                   // sub-phase ticks on (TSW_PLAN_DEBUG)
 };
 
 size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks);

@@ -294,6 +294,16 @@ __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
 
 }  // namespace
 
+// diagnostics: wall-clock ticks of sub-phases (P.sec_ticks[8..15], printed by TSW_PLAN_DEBUG)
+#define PLAN_TICK(slot)                              \
+  do {                                               \
+    if (P.dbg && tid == 0) {                         \
+      const unsigned long long nw_ = wall_clock64(); \
+      s_tick[slot] += nw_ - s_tp;                    \
+      s_tp = nw_;                                    \
+    }                                                \
+  } while (0)
+
 template <bool AG, bool OC>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
@@ -301,7 +311,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   __shared__ uint32_t s_q, s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
-  __shared__ unsigned long long s_tick[8], s_tlast;
+  __shared__ unsigned long long s_tick[16], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
   const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6, nwaves = bd >> 6;
   const uint32_t n = P.n, W = P.W;
@@ -374,7 +384,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_ctl.status = PLAN_RUNNING;
     s_exit = 0;
     s_q = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
-    for (int k = 0; k < 8; ++k) s_tick[k] = 0;
+    for (int k = 0; k < 16; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
   }
@@ -514,8 +524,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // s — terminal until now — gains one out-edge, so the only new cycle possible is
       // one through s. CANDC[k] prefetches s's next hop toward k's goal for every rule-3
       // candidate k, so a swap needs no global round trip on the serial path.
+      if (P.dbg && tid == 0) s_tp = wall_clock64();
       rules_init(P, S);
       if (P.prefetch) rules_prefetch(P, S, &s_q);
+      PLAN_TICK(15);
       for (;;) {
         const uint32_t cursor = s_ctl.i;
         uint32_t best = NO_AGENT;
@@ -530,6 +542,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         best = wave_min_u32(best);
         if (lane == 0) s_wcount[wid] = best;
         __syncthreads();
+        PLAN_TICK(13);
         if (tid == 0) {
           uint32_t b = NO_AGENT;
           for (uint32_t w = 0; w < nwaves; ++w) b = s_wcount[w] < b ? s_wcount[w] : b;
@@ -595,6 +608,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           }
         }
         __syncthreads();
+        PLAN_TICK(14);
         if (s_best == NO_AGENT) break;
         if (s_miss) {
           // goals of the fired agents changed: their next hops (hence succ) must be looked up
@@ -610,6 +624,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           }
           rules_init(P, S);
           if (P.prefetch) rules_prefetch(P, S, &s_q);
+          PLAN_TICK(15);
         }
       }
       if (s_exit) break;
@@ -649,6 +664,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (tid == 0) {
           s_miss = 0;
           s_ctl.move_rounds += 1;
+          if (P.dbg) s_tp = wall_clock64();
         }
         __syncthreads();
         // A: target cell of every open agent; reset MU at its target and its own cell
@@ -670,12 +686,14 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           S.MU[v] = NO_AGENT;
         }
         open = __syncthreads_or(open);
+        PLAN_TICK(8);
         if (!open) break;
         if (s_miss) break;  // exit to K3 below
         // B: lowest open agent targeting each cell
         for (uint32_t k = tid; k < n; k += bd)
           if (S.DEC[k] == DEC_OPEN) atomicMin(&S.MU[S.SUCC[k]], k);
         __syncthreads();
+        PLAN_TICK(9);
         // C: lowest open agent whose cell is wanted by an open mutual partner below it
         uint32_t sp = NO_AGENT;
         for (uint32_t k = tid; k < n; k += bd) {
@@ -698,6 +716,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         }
         __syncthreads();
         const uint32_t spmin = s_best;
+        PLAN_TICK(10);
         // D: decide (reads the round-start state only)
         for (uint32_t k = tid; k < n && k < spmin; k += bd) {
           if (S.DEC[k] != DEC_OPEN) continue;
@@ -732,6 +751,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           S.DEC[k] = act;
         }
         __syncthreads();
+        PLAN_TICK(11);
         // E: commit (disjoint cells by construction)
         for (uint32_t k = tid; k < n; k += bd) {
           const uint8_t d = S.DEC[k];
@@ -755,6 +775,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           }
         }
         __syncthreads();
+        PLAN_TICK(12);
         if (s_miss) break;
       }
       if (s_miss) {
@@ -833,7 +854,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     P.ctl->err |= err;
     s_tick[s_tsec] += wall_clock64() - s_tlast;
     if (P.sec_ticks)
-      for (int k = 0; k < 8; ++k) P.sec_ticks[k] += s_tick[k];
+      for (int k = 0; k < 16; ++k) P.sec_ticks[k] += s_tick[k];
   }
 }
 
