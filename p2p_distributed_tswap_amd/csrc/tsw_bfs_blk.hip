@@ -195,6 +195,76 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       }
     };
 
+    // ---- lane pairs: a block is processed by lanes (2j, 2j+1), lane h = lane & 1 owning its
+    // rows 4h..4h+3 as one dword (rows of 8 cells = bytes). All bit logic is 32-bit; the two
+    // halves exchange their rows with a DPP quad_perm swap (no LDS). A level's ~30 active
+    // blocks fill the wave's 64 lanes instead of leaving half of them idle.
+    const uint32_t h = lane & 1u;
+    uint32_t* V32 = reinterpret_cast<uint32_t*>(V);
+    const uint32_t* FR32 = reinterpret_cast<const uint32_t*>(FRs);
+    unsigned int* WL32 = reinterpret_cast<unsigned int*>(WL);
+    constexpr uint32_t C0 = 0x01010101u, C7 = 0x80808080u;
+    auto partner = [](uint32_t x) -> uint32_t {  // value of the other lane of the pair
+      return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    };
+    // run-start anchors among this half's new cells (block's run starts numbered in block order)
+    auto anchors2 = [&](uint32_t p, uint32_t nw, uint32_t f0, uint32_t fw, uint32_t lvl) {
+      const uint32_t bx = p - __umulhi(p, A.bp_magic) * Bp;
+      const uint32_t wf = ((f0 << 1) & ~C0) | ((bx & 3u) ? ((fw >> 7) & C0) : 0u);
+      const uint32_t rs = f0 & ~wf;
+      const uint32_t below = __popc(partner(rs));  // the low half's run starts precede ours
+      uint32_t rsn = nw & rs;
+      const uint32_t base = AB[p] + (h ? below : 0u);
+      while (rsn) {
+        const uint32_t bb = (uint32_t)__builtin_ctz(rsn);
+        anch[base + __popc(rs & ((1u << bb) - 1u))] = (uint16_t)lvl;
+        rsn &= rsn - 1u;
+      }
+    };
+    // exact pushes of block p (this lane's half has new cells nw): the blocks gaining a cell at
+    // lvl + 1 — self (either half, or across the halves), W / E (either half), N (row 0, even
+    // lane), S (row 7, odd lane); dedup by test-and-set on the next level's flags, appends by
+    // ballot + mbcnt. Even lanes own (self, W, N), odd lanes (E, S).
+    auto push2 = [&](uint32_t p, uint32_t nw, uint32_t vv, uint32_t f0, uint32_t fw, uint32_t fe, uint32_t fx,
+                    uint32_t fp, uint32_t vw, uint32_t ve, uint32_t vx, uint32_t vp, uint32_t* Fn, uint16_t* Ln,
+                    uint16_t* On) {
+      const uint32_t in = ((nw << 1) & ~C0) | ((nw >> 1) & ~C7) | (nw << 8) | (nw >> 8);
+      const uint32_t cross = h ? (nw << 24) : (nw >> 24);  // row 4 -> row 3 / row 3 -> row 4
+      const bool s_self = ((in & f0 & ~vv) | (cross & fp & ~vp)) != 0u;
+      const bool s_w = (((nw & C0) << 7) & fw & ~vw) != 0u;
+      const bool s_e = (((nw & C7) >> 7) & fe & ~ve) != 0u;
+      const bool s_x = ((h ? (nw >> 24) : (nw << 24)) & fx & ~vx) != 0u;  // S (odd) / N (even)
+      const uint32_t both = (s_self ? 1u : 0u) | (s_w ? 2u : 0u) | (s_e ? 4u : 0u);
+      const uint32_t pb = both | partner(both);
+      const uint32_t tw = p - 1u, te = p + 1u, tx = h ? p + Bp : p - Bp;
+      // even: self, W, N; odd: E, S
+      bool w0 = h ? (pb & 4u) != 0u : (pb & 1u) != 0u;
+      bool w1 = h ? s_x : (pb & 2u) != 0u;
+      bool w2 = h ? false : s_x;
+      const uint32_t t0 = h ? te : p, t1 = h ? tx : tw, t2 = tx;
+      auto tas2 = [&](bool w, uint32_t t) -> uint32_t {
+        const uint32_t m = w ? 1u << (t >> klog) : 0u;
+        return atomicOr(&Fn[w ? (t & kmask) : lane], m) & m;
+      };
+      const uint32_t o0 = tas2(w0, t0), o1 = tas2(w1, t1), o2 = tas2(w2, t2);
+      w0 = w0 && !o0;
+      w1 = w1 && !o1;
+      w2 = w2 && !o2;
+      const bool lds_only = nn + 3u * 64u <= cap;
+      auto append2 = [&](bool c, uint32_t entry) {
+        const uint64_t m = __ballot(c);
+        if (c) {
+          const uint32_t pos = nn + lane_rank(m);
+          if (lds_only) Ln[pos] = (uint16_t)entry;
+          else blk_list_put_slow(Ln, On, cap, pos, entry);
+        }
+        nn += (uint32_t)__popcll(m);
+      };
+      append2(w0, t0);
+      append2(w1, t1);
+      append2(w2, t2);
+    };
+
     // ---- level 0: the goal cell; queue the blocks that gain cells at distance 1 ----------
     uint32_t ncur = 0;
     {
@@ -230,6 +300,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       uint32_t* Fn = FL + nxt * nfk;
       const uint64_t pnew = ((gpar + lvl) & 1u) ? ~CB_EVEN : CB_EVEN;  // cells at distance lvl
       const uint64_t psrc = ~pnew;                                      // cells at distance lvl-1
+      const uint32_t psrc2 = (uint32_t)psrc;  // a half-block has the same checkerboard
       nn = 0;
       // one chunk: lane's list entry p (idle lanes: the guard block idle_p, act = false)
       auto chunk = [&](uint32_t p, bool act) {
@@ -250,7 +321,34 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         push(p, nw, vv, f0, fw, fe, fn, fs, vw, ve, vn, vs, Fn, Ln, On);
         ++n_chunk;
       };
-      if (ncur <= cap) {
+      // one chunk of 32 blocks: this lane's half of entry p (idle lanes: the guard block)
+      auto chunk2 = [&](uint32_t p, bool act) {
+        const uint32_t o = 2u * p + h;
+        const uint32_t ox = h ? 2u * (p + Bp) : 2u * (p - Bp) + 1u;  // vertical neighbour dword
+        const uint32_t v0 = V32[o], vw = V32[o - 2u], ve = V32[o + 2u], vx = V32[ox];
+        const uint32_t f0 = FR32[o], fw = FR32[o - 2u], fe = FR32[o + 2u], fx = FR32[ox];
+        const uint32_t vp = partner(v0), fp = partner(f0);
+        const uint32_t a = v0 & psrc2, aw = vw & psrc2, ae = ve & psrc2, ax = vx & psrc2, ap = vp & psrc2;
+        const uint32_t up_in = h ? (ap >> 24) : (ax >> 24);   // row above the half's top row
+        const uint32_t dn_in = h ? (ax << 24) : (ap << 24);   // row below the half's bottom row
+        const uint32_t ex = ((a << 1) & ~C0) | ((a >> 1) & ~C7) | ((aw >> 7) & C0) | ((ae << 7) & C7) | (a << 8) |
+                            (a >> 8) | up_in | dn_in;
+        const uint32_t nw = ex & f0 & ~v0;  // 0 for idle lanes (FR of the guard block is 0)
+        const uint32_t vv = v0 | nw;
+        V32[o] = vv;  // owner-exclusive (deduplicated list, one lane per half); idle lanes rewrite 0
+        const uint32_t wln = nw & (((v0 << 1) & ~C0) | ((vw >> 7) & C0));
+        if (wln) atomicOr(WL32 + o, wln);
+        const uint32_t nwp = partner(nw);
+        bad |= act && (nw | nwp) == 0u;  // entries must gain a cell
+        anchors2(p, nw, f0, fw, lvl);
+        push2(p, nw, vv, f0, fw, fe, fx, fp, vw, ve, vx, vp, Fn, Ln, On);
+        ++n_chunk;
+      };
+      if (ncur <= 32u && ncur <= cap) {
+        // few active blocks: lane pairs, one half-block per lane (a single chunk)
+        const uint32_t j0 = lane >> 1;
+        chunk2(j0 < ncur ? (uint32_t)Lc[j0] : idle_p, j0 < ncur);
+      } else if (ncur <= cap) {
         // LDS-only list (wave-uniform): no global load in the loop, so nothing waits for the
         // wave's outstanding anchor stores; entries prefetched one chunk ahead
         uint32_t e_next = lane < ncur ? (uint32_t)Lc[lane] : idle_p;

@@ -1,5 +1,4 @@
 set -o pipefail
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_golden.py -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_par.log 2>&1 &&
-timeout -k 10 300 python -u scripts/scale_bench.py c3 --cpu-steps 2 > gpurun_out/scale.log 2>&1 &&
-timeout -k 10 400 python -u scripts/scale_bench.py wh10k --max-t 30 --cpu-steps 2 >> gpurun_out/scale.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bfs.py > gpurun_out/bfs_tests.log 2>&1 && \
+TSW_BFS_PROF=1 timeout -k 10 120 python scripts/bfs_bench.py 10000 3 > gpurun_out/bfs_bench.log 2>&1
