@@ -114,7 +114,7 @@ struct tsw_ctx {
   uint8_t* d_candc = nullptr;
   uint32_t* d_f1 = nullptr;
   uint32_t* d_f2 = nullptr;
-  uint32_t* d_mu = nullptr;
+  uint64_t* d_mu = nullptr;
   uint32_t* d_dups = nullptr;
   uint32_t* h_dups = nullptr;  // pinned
   uint8_t* d_st = nullptr;
@@ -609,7 +609,7 @@ int ensure_agents(tsw_ctx* c, size_t n) {
   if (!c->d_occ) {
     HIPCHK(hipMalloc(&c->d_occ, (size_t)c->G.ncell * 4));
     HIPCHK(hipMalloc(&c->d_cnt, (size_t)c->G.ncell * 4));
-    HIPCHK(hipMalloc(&c->d_mu, (size_t)c->G.ncell * 4));
+    HIPCHK(hipMalloc(&c->d_mu, (size_t)c->G.ncell * 8));
     HIPCHK(hipMalloc(&c->d_dups, 4));
     HIPCHK(hipHostMalloc(&c->h_dups, 4, hipHostMallocDefault));
   }

@@ -58,7 +58,7 @@ struct PlanArgs {
   uint32_t* f2;
   uint32_t* ap;   // rule-4 cycle members
   uint32_t* occ;  // per cell occupancy
-  uint32_t* mu;   // per cell lowest undecided targeting agent (global copy)
+  uint64_t* mu;   // per cell round-tagged lowest undecided targeting agent (global copy)
   const uint32_t* pick_xy;
   const uint32_t* pick;
   const uint32_t* dlv;

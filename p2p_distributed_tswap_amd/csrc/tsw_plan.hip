@@ -18,9 +18,10 @@
 //   MOVE    movement phase (tswap.rs:257-285), exact, as decidability rounds: agent k
 //           commits in a round iff no still-undecided agent a < k can change what k reads
 //           at its turn in the sequential scan — a's target is neither k's target nor
-//           k's cell, a is not the occupant of k's target, and no undecided agent below
-//           k is a pending mutual-swap partner (so no undecided position moves before its
-//           own turn). Decisions read the round-start state, commits are disjoint.
+//           k's cell and a is not the occupant of k's target (a mutual-swap partner of a
+//           lower undecided agent is caught by the second test). Decisions read the
+//           round-start state, commits are disjoint. Three passes per round: targets +
+//           round-tagged MU (lowest undecided agent per target cell), decide, commit.
 //           With duplicate start cells the phase runs as the serial scan instead.
 //   RECORD  parallel (Point, AgentState) record (tswap.rs:144-158) + termination (:163-169)
 // When a next hop is unresolved (lazy next-hop mode) the kernel enqueues every such
@@ -87,7 +88,7 @@ struct Arrays {
   uint32_t* F1;    // rules: pointer-doubling buffers (n + 1 entries, n = terminal sink)
   uint32_t* F2;
   uint32_t* OCC;   // per cell: lowest agent | OCC_FLAG, or OCC_NONE
-  uint32_t* MU;    // per cell: lowest undecided agent targeting it (movement rounds)
+  uint64_t* MU;    // per cell: (round << 32) | ~(lowest undecided agent targeting it), movement rounds
   const uint32_t* PXY;
   uint8_t* USED;
 };
@@ -350,7 +351,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   }
   if constexpr (OC) {
     S.OCC = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
-    S.MU = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
+    S.MU = reinterpret_cast<uint64_t*>(carve((size_t)P.ncell * 8));
   } else {
     S.OCC = P.occ;
     S.MU = P.mu;
@@ -379,6 +380,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   }
   if constexpr (OC)
     for (uint32_t c = tid; c < P.ncell; c += bd) S.OCC[c] = P.occ[c];
+  // round tags start at 1 (move_rounds is incremented before use), so zeroed MU is stale
+  for (uint32_t c = tid; c < P.ncell; c += bd) S.MU[c] = 0ull;
   if (tid == 0) {
     s_ctl = *P.ctl;
     s_ctl.status = PLAN_RUNNING;
@@ -663,11 +666,17 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       for (;;) {
         if (tid == 0) {
           s_miss = 0;
+          s_best = NO_AGENT;
           s_ctl.move_rounds += 1;
           if (P.dbg) s_tp = wall_clock64();
         }
         __syncthreads();
-        // A: target cell of every open agent; reset MU at its target and its own cell
+        // Within a round DEC only goes OPEN -> {STAY, MOVE, SWAP} (own entry, pass 2) and the
+        // commit pass turns those into DONE (or back to OPEN), so "open at round start" reads
+        // as DEC != DEC_DONE for every other agent throughout the round.
+        const uint64_t tag = (uint64_t)s_ctl.move_rounds << 32;
+        // pass 1: target cell of every open agent; MU[c] = lowest open agent targeting c, as
+        // a round-tagged max of ~k (no reset pass: entries of older rounds are stale)
         int open = 0;
         for (uint32_t k = tid; k < n; k += bd) {
           if (S.DEC[k] != DEC_OPEN) continue;
@@ -680,50 +689,39 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             S.SUCC[k] = NO_CELL;
             continue;
           }
-          const uint32_t v = S.V[k], u = step_cell(v, (uint32_t)code, W);
+          const uint32_t u = step_cell(S.V[k], (uint32_t)code, W);
           S.SUCC[k] = u;
-          S.MU[u] = NO_AGENT;
-          S.MU[v] = NO_AGENT;
+          atomicMax(reinterpret_cast<unsigned long long*>(&S.MU[u]), (unsigned long long)(tag | (uint32_t)~k));
         }
         open = __syncthreads_or(open);
         PLAN_TICK(8);
         if (!open) break;
         if (s_miss) break;  // exit to K3 below
-        // B: lowest open agent targeting each cell
-        for (uint32_t k = tid; k < n; k += bd)
-          if (S.DEC[k] == DEC_OPEN) atomicMin(&S.MU[S.SUCC[k]], k);
-        __syncthreads();
-        PLAN_TICK(9);
-        // C: lowest open agent whose cell is wanted by an open mutual partner below it
-        uint32_t sp = NO_AGENT;
+        auto mu_of = [&](uint32_t c) -> uint32_t {  // lowest open agent targeting c this round
+          const uint64_t x = S.MU[c];
+          return (x >> 32) == (tag >> 32) ? ~(uint32_t)x : NO_AGENT;
+        };
+        // pass 2: tentatively decide every open agent whose turn can be replayed from the
+        // round-start state. What k reads at its turn is OCC[u] (u = its target), the
+        // occupant j's cell, goal and next hop, and its own cell; an undecided agent a < k
+        // changes one of them only by targeting u (MU[u] != k), by being the occupant (j < k
+        // still open) or by targeting k's cell (MU[v] < k). That alone is not enough: an
+        // open agent k whose open occupant b < k is its mutual-swap partner is carried to
+        // b's cell before its turn and then targets a cell nobody can name yet, so no agent
+        // above the lowest such k (s_best) may commit this round. The same pass finds it.
         for (uint32_t k = tid; k < n; k += bd) {
           if (S.DEC[k] != DEC_OPEN) continue;
-          const uint32_t o = S.OCC[S.SUCC[k]];
-          if (o == OCC_NONE) continue;
-          const uint32_t b = o & OCC_IDX;
-          if (b < k && S.DEC[b] == DEC_OPEN && S.SUCC[b] == S.V[k]) {
-            sp = k;
-            break;
-          }
-        }
-        sp = wave_min_u32(sp);
-        if (lane == 0) s_wcount[wid] = sp;
-        __syncthreads();
-        if (tid == 0) {
-          uint32_t b = NO_AGENT;
-          for (uint32_t w = 0; w < nwaves; ++w) b = s_wcount[w] < b ? s_wcount[w] : b;
-          s_best = b;
-        }
-        __syncthreads();
-        const uint32_t spmin = s_best;
-        PLAN_TICK(10);
-        // D: decide (reads the round-start state only)
-        for (uint32_t k = tid; k < n && k < spmin; k += bd) {
-          if (S.DEC[k] != DEC_OPEN) continue;
           const uint32_t u = S.SUCC[k], v = S.V[k];
-          if (S.MU[u] != k) continue;
-          if (S.MU[v] < k) continue;
           const uint32_t o = S.OCC[u];
+          if (o != OCC_NONE) {
+            const uint32_t b = o & OCC_IDX;
+            if (b < k && S.DEC[b] != DEC_DONE && S.SUCC[b] == v) {
+              atomicMin(&s_best, k);
+              continue;
+            }
+          }
+          if (mu_of(u) != k) continue;
+          if (mu_of(v) < k) continue;
           uint8_t act;
           if (o == OCC_NONE) {
             act = DEC_MOVE;  // rule 2
@@ -732,8 +730,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             if (j == k) {
               act = DEC_STAY;
             } else {
-              const uint8_t dj = S.DEC[j];
-              if (j < k && dj != DEC_DONE) continue;  // occupant still open below k
+              if (j < k && S.DEC[j] != DEC_DONE) continue;  // occupant still open below k
               if (S.V[j] == S.G[j]) {
                 act = DEC_STAY;
               } else {
@@ -751,11 +748,16 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           S.DEC[k] = act;
         }
         __syncthreads();
-        PLAN_TICK(11);
-        // E: commit (disjoint cells by construction)
+        PLAN_TICK(10);
+        // pass 3: commit below s_best (disjoint cells by construction); undo the rest
+        const uint32_t spmin = s_best;
         for (uint32_t k = tid; k < n; k += bd) {
           const uint8_t d = S.DEC[k];
           if (d < DEC_STAY) continue;
+          if (k >= spmin) {
+            S.DEC[k] = DEC_OPEN;
+            continue;
+          }
           S.DEC[k] = DEC_DONE;
           if (d == DEC_STAY) continue;
           const uint32_t u = S.SUCC[k], v = S.V[k];
@@ -885,7 +887,7 @@ size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool 
   auto r16 = [](size_t b) { return (b + 15u) & ~(size_t)15u; };
   size_t b = r16(1024 * 4);
   if (agents) b += 4 * r16((size_t)n * 4) + 2 * r16((size_t)(n + 1) * 4) + 4 * r16(n);
-  if (occ) b += 2 * r16((size_t)ncell * 4);
+  if (occ) b += r16((size_t)ncell * 4) + r16((size_t)ncell * 8);
   if (tasks) b += r16((size_t)m * 4) + r16(m);
   return b;
 }

@@ -1,3 +1,4 @@
 set -o pipefail
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_10k -o run -- python3 scripts/scale_bench.py wh10k --max-t 30 --cpu-steps 1 > gpurun_out/prof_10k.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 120 python bench.py --steps 2 --warmup 1 --no-bfs --no-cpu > gpurun_out/bench_plan.json 2> gpurun_out/bench_plan.err
