@@ -1,4 +1,4 @@
 set -o pipefail
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bfs.py > gpurun_out/bfs_tests.log 2>&1 && \
-TSW_BFS_PROF=1 timeout -k 10 120 python scripts/bfs_bench.py 10000 3 > gpurun_out/bfs_bench.log 2>&1
+TSW_PLAN_DEBUG=1 timeout -k 10 120 python bench.py --steps 1 --warmup 0 --no-bfs --no-cpu > gpurun_out/dbg.json 2> gpurun_out/dbg.log && \
+bash scripts/profile_round.sh r1
