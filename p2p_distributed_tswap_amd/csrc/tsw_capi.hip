@@ -35,6 +35,7 @@ struct DevStatus {
   uint32_t done;
   uint32_t qcount;
   uint32_t novf;  // LDS A*: queries handed to the global-heap kernel
+  uint32_t novf2;  // second tier (LDS heap, global g_scores): queries handed on to k_astar
   uint32_t work;  // k_bfs_wave goal dequeue counter
 };
 
@@ -88,6 +89,7 @@ struct tsw_ctx {
   uint16_t* d_gs16 = nullptr;
   uint32_t* d_ep16 = nullptr;
   AstarQuery* d_ovf = nullptr;
+  AstarQuery* d_ovf2 = nullptr;  // second-tier overflow list (same capacity as d_ovf)
   size_t ovf_cap = 0;
 
   // query queue
@@ -345,19 +347,33 @@ int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint
                           c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
   } else {
     // one query per wave, LDS heap; the g_score slots are shared with k_astar (same tag scheme)
-    if (nq > c->ovf_cap) {
+    if (nq > c->ovf_cap || !c->d_ovf2) {
       HIPCHK(hipStreamSynchronize(c->s));
+      size_t cap2 = c->ovf_cap;
       HIPCHK(dgrow(c->d_ovf, c->ovf_cap, nq));
+      HIPCHK(dgrow(c->d_ovf2, cap2, c->ovf_cap));
     }
-    HIPCHK(hipMemsetAsync(&c->d_stat->novf, 0, 4, c->s));
+    HIPCHK(hipMemsetAsync(&c->d_stat->novf, 0, 8, c->s));  // novf, novf2
     const uint32_t slots = std::min(astar_wave_slots(c->G, c->num_cu), c->nslots);
     HIPCHK(launch_astar_wave(c->G, Q, nq, nh, c->tstride, res, lens, c->d_gs, c->d_epochs, slots, c->d_ovf,
-                             &c->d_stat->novf, c->wave_hcap, c->s));
+                             &c->d_stat->novf, c->wave_hcap, false, c->s));
     HIPCHK(hipMemcpyAsync(&c->h_stat->novf, &c->d_stat->novf, 4, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
-    const uint32_t novf = c->h_stat->novf;
+    uint32_t novf = c->h_stat->novf;
+    AstarQuery* rest = c->d_ovf;
+    if (novf && astar_wave_lds_gs(c->G) && !getenv("TSW_ASTAR_NO_TIER2")) {
+      // second tier: g_scores that outgrew the LDS encoding (byte words: detours > 62) move to
+      // the global u32 slots while the heap stays in LDS; only heap overflows reach k_astar
+      const uint32_t slots2 = std::min(astar_wave_slots(c->G, c->num_cu, true), c->nslots);
+      HIPCHK(launch_astar_wave(c->G, c->d_ovf, novf, nh, c->tstride, res, lens, c->d_gs, c->d_epochs, slots2,
+                               c->d_ovf2, &c->d_stat->novf2, c->wave_hcap, true, c->s));
+      HIPCHK(hipMemcpyAsync(&c->h_stat->novf2, &c->d_stat->novf2, 4, hipMemcpyDeviceToHost, c->s));
+      HIPCHK(hipStreamSynchronize(c->s));
+      novf = c->h_stat->novf2;
+      rest = c->d_ovf2;
+    }
     if (novf)
-      HIPCHK(launch_astar(c->G, c->d_ovf, nullptr, novf, novf, nh, c->tstride, res, lens, c->d_heaps, c->hcap,
+      HIPCHK(launch_astar(c->G, rest, nullptr, novf, novf, nh, c->tstride, res, lens, c->d_heaps, c->hcap,
                           c->d_gs, c->d_epochs, c->nslots, &c->d_stat->err, c->s));
   }
   c->st.astar_queries += nq;
@@ -976,7 +992,7 @@ void tsw_destroy(tsw_ctx* c) {
   };
   fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_frb); fre(c->d_abase); fre(c->d_wlg); fre(c->d_anch); fre(c->d_lovf); fre(c->d_bprof); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
-  fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf);
+  fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf); fre(c->d_ovf2);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
   fre(c->d_gt); fre(c->d_dec); fre(c->d_mu); fre(c->d_dups); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
   if (c->h_dups) (void)hipHostFree(c->h_dups);

@@ -14,7 +14,9 @@
 // Launch wrappers are plain C++ functions declared in tsw_launch.h.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "tsw_internal.h"
 #include "tsw_launch.h"
@@ -678,6 +680,198 @@ __device__ __forceinline__ uint8_t astar_wave_core(const DevGrid& G, uint32_t v,
 }
 
 // ----------------------------------------------------------------------------
+// Wave-cooperative A* core (k_astar_wave default; TSW_ASTAR_SERIAL=1 selects the lone-lane
+// core above). Same BinaryHeap algorithm, same heap contents after every operation — only the
+// way each sift touches its path changes, so the pop order (and every label) is identical:
+//  * sift_down_to_bottom: the 62 descendants of the hole within 5 levels are read by one
+//    ds_read (lane j -> depth k = log2(j + 2), index j + 2 - 2^k below the hole). Each left
+//    child compares its key with its sibling's (DPP lane swap); "take the right child" bits and
+//    the node-exists bits are balloted, and the path (left <= right -> right child, a lone left
+//    child is taken, stop at a childless node) is walked in SALU. The path's values move up one
+//    level with one ds_write. A 4096-entry heap has depth 12: <= 3 LDS round trips per pop
+//    instead of 12 dependent ones.
+//  * sift_up (of the popped-last element and of every push): the hole's ancestors are read one
+//    per lane. The root path is heap ordered, so the ancestors whose key exceeds the element's
+//    (those the element passes: it stops at the first parent it is not smaller than) are a
+//    suffix of it: one ballot gives the landing depth and one ds_write shifts them down.
+//  * the four neighbours are relaxed by lanes 0..3 at once (distinct cells); the improved
+//    ones are pushed in direction order (tswap.rs:337-360's loop order).
+// LDS instructions of one wave complete in issue order, so a lane reads what another lane of
+// the same wave wrote by an earlier instruction.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rl32(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t l) {
+  return ((uint64_t)rl32((uint32_t)(x >> 32), l) << 32) | rl32((uint32_t)x, l);
+}
+__device__ __forceinline__ void wave_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// BinaryHeap::sift_up(0, pos) with `elem` in the hole; wave-uniform arguments.
+__device__ __forceinline__ void wsift_up(uint64_t* Hp, uint32_t pos, uint64_t elem, uint32_t lane) {
+  const uint32_t dp = 31u - (uint32_t)__builtin_clz(pos + 1u);  // depth of the hole (root = 0)
+  const uint32_t k = hk(elem);
+  uint64_t a = 0;
+  bool gt = false;
+  if (lane < dp) {
+    a = Hp[((pos + 1u) >> (dp - lane)) - 1u];  // ancestor at depth `lane`
+    gt = k < hk(a);                             // elem moves past it
+  }
+  const uint32_t t = dp - (uint32_t)__popcll(__ballot(gt));  // landing depth
+  wave_order();
+  if (lane >= t && lane < dp) Hp[((pos + 1u) >> (dp - lane - 1u)) - 1u] = a;  // one level down the path
+  else if (lane == dp) Hp[((pos + 1u) >> (dp - t)) - 1u] = elem;
+  wave_order();
+}
+
+// BinaryHeap::pop (swap last into the root, sift_down_to_bottom(0), sift_up(0, hole)); len >= 1.
+__device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t lane) {
+  const uint32_t end = --len;
+  uint32_t pos = 0;
+  uint64_t last = 0, top = 0;
+  const uint32_t kk = 31u - (uint32_t)__builtin_clz(lane + 2u);  // window depth of this lane (lane < 62)
+  const uint32_t ki = lane + 2u - (1u << kk);
+  for (bool first = true;; first = false) {
+    uint32_t node = 0;
+    bool valid = false;
+    if (lane < 62u) {
+      node = ((pos + 1u) << kk) - 1u + ki;
+      valid = node < end;
+    }
+    uint64_t val = 0;
+    if (valid) val = Hp[node];
+    else if (first && lane >= 62u) val = Hp[lane == 62u ? end : 0u];
+    if (first) {
+      last = rl64(val, 62);
+      top = rl64(val, 63);
+      if (end == 0) return last;
+    }
+    const uint32_t key = hk(val);
+    const uint32_t sib = (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    const uint64_t VL = __ballot(valid);
+    const uint64_t CR = __ballot(valid && !(lane & 1u) && node + 1u < end && key >= sib);
+    uint32_t idx = 0, d = 0;
+    uint64_t on = 0;
+#pragma unroll
+    for (uint32_t k = 1; k <= 5; ++k) {
+      const uint32_t ll = (1u << k) - 2u + 2u * idx;  // lane of the left child
+      if (!((VL >> ll) & 1ull)) break;
+      const uint32_t b = (uint32_t)((CR >> ll) & 1ull);
+      idx = 2u * idx + b;
+      on |= 1ull << (ll + b);
+      d = k;
+    }
+    if (d == 0) break;
+    wave_order();
+    if ((on >> lane) & 1ull) Hp[(node - 1u) >> 1] = val;  // move up into the parent
+    wave_order();
+    pos = ((pos + 1u) << d) - 1u + idx;
+    if (d < 5) break;
+  }
+  wsift_up(Hp, pos, last, lane);
+  return top;
+}
+
+// FB: the grid's free-cell row bitmap (DevGrid::freebits) staged in LDS, so relaxing a node
+// needs no global load (a dependent L2 round trip per pop was the kernel's critical path).
+template <int GSM>
+__device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag,
+                                                  uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
+                                                  const uint32_t* FB, int32_t* len_out, uint32_t* pops_out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t pops = 0;
+  const uint32_t W = G.W, H = G.H, Ww = G.Ww;
+  const uint32_t vy = v / W, vx = v - vy * W, gy = goal / W, gx = goal - gy * W;
+  if (v == goal) {
+    *len_out = 1;
+    return NH_STAY;
+  }
+  const uint32_t tagw = tag << 22;
+  const uint32_t h0 = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
+  if (h0 >= (1u << 17)) {
+    *len_out = -2;
+    return NH_UNKNOWN;
+  }
+  if (lane == 0) {
+    if constexpr (GSM == 2) GB[v] = 0x80u;
+    else GS[v] = tagw;
+    Hp[0] = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
+  }
+  wave_order();
+  uint32_t len = 1;
+  // lanes 0..3 own the neighbour in direction `lane` (S, E, N, W: tswap.rs:62-73)
+  const uint32_t dd = lane & 3u;
+  while (len > 0) {
+    ++pops;
+    *pops_out = pops;
+    const uint64_t e = wpop(Hp, len, lane);
+    const uint32_t cx = (uint32_t)(e >> 16) & 0xFFFFu, cy = (uint32_t)e & 0xFFFFu;
+    const uint32_t cg = hk(e) & 0x7FFFu;
+    const uint32_t c = cy * W + cx;
+    if (c == goal) {
+      *len_out = (int32_t)cg + 1;
+      if constexpr (GSM == 2) return (uint8_t)((GB[goal] >> 5) & 3u);
+      else return (uint8_t)((GS[goal] >> 20) & 3u);
+    }
+    uint32_t labc;
+    if constexpr (GSM == 2) labc = (GB[c] >> 5) & 3u;
+    else labc = (GS[c] >> 20) & 3u;
+    const uint32_t tg = cg + 1u;
+    bool imp = false, ovf = false;
+    uint64_t ent = 0;
+    // neighbour of lane dd (unsigned wrap: x - 1 at x = 0 fails the bound test)
+    const uint32_t nx = dd == 1 ? cx + 1 : (dd == 3 ? cx - 1 : cx);
+    const uint32_t ny = dd == 0 ? cy + 1 : (dd == 2 ? cy - 1 : cy);
+    const uint32_t nc = ny * W + nx;
+    uint32_t fw = 0, old = 0;
+    if (lane < 4u && nx < W && ny < H) {  // both LDS reads issue together
+      fw = FB[ny * Ww + (nx >> 5)];
+      if constexpr (GSM == 2) old = GB[nc];
+      else old = GS[nc];
+    }
+    if ((fw >> (nx & 31u)) & 1u) {
+      uint32_t oldg, man = 0;
+      if constexpr (GSM == 2) {
+        man = (nx > vx ? nx - vx : vx - nx) + (ny > vy ? ny - vy : vy - ny);
+        oldg = (old & 0x80u) ? man + 2u * (old & 31u) : 0xFFFFFFFFu;
+      } else {
+        oldg = ((old & 0xFFC00000u) == tagw) ? (old & GS_G_MASK) : 0xFFFFFFFFu;
+      }
+      if (tg < oldg) {
+        imp = true;
+        const uint32_t lab = cg == 0 ? dd : labc;
+        const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
+        const uint32_t f = tg + h;
+        ovf = tg >= (1u << 15) || f >= (1u << 17);
+        if constexpr (GSM == 2) {
+          const uint32_t hh = (tg - man) >> 1;
+          ovf = ovf || hh > 31u;
+          if (!ovf) GB[nc] = (uint8_t)(0x80u | (lab << 5) | hh);
+        } else {
+          if (!ovf) GS[nc] = tagw | (lab << 20) | tg;
+        }
+        ent = ((uint64_t)((f << 15) | tg) << 32) | (nx << 16) | ny;
+      }
+    }
+    uint64_t M = __ballot(imp);
+    if (__ballot(ovf) != 0ull || len + (uint32_t)__popcll(M) > hcap) {
+      *len_out = -2;
+      return NH_UNKNOWN;
+    }
+    wave_order();
+    while (M) {
+      const uint32_t d = (uint32_t)__builtin_ctzll(M);
+      M &= M - 1ull;
+      wsift_up(Hp, len, rl64(ent, d), lane);
+      ++len;
+    }
+  }
+  *len_out = 2;
+  return fallback_code(G.nbmask[v], vx, vy, gx, gy);
+}
+
+// ----------------------------------------------------------------------------
 // K3 (grids of > 1024 cells): the same exact A* (astar_one), ONE QUERY PER WAVE with the heap
 // in LDS and, when the grid fits (WAVE_GS_LDS_MAX cells), the g_score words in LDS too. The
 // planner's lazy mode exits to the host whenever a step needs unresolved next hops, so K3
@@ -690,13 +884,20 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
                                                    uint8_t* __restrict__ res, int32_t* __restrict__ lens,
                                                    uint32_t hcap, uint32_t gs_lds, uint32_t* __restrict__ gs_all,
                                                    uint32_t* __restrict__ epochs, AstarQuery* __restrict__ ovf,
-                                                   uint32_t* __restrict__ novf) {
+                                                   uint32_t* __restrict__ novf, uint32_t serial,
+                                                   unsigned long long* __restrict__ prof) {
   extern __shared__ __align__(16) uint64_t wsm[];
   uint64_t* Hp = wsm;
   const uint32_t lane = threadIdx.x, ncell = G.ncell;
   // gs_lds: 0 = u32 g_scores in global slots, 1 = u32 in LDS, 2 = bytes in LDS (astar_one_b8)
   uint32_t* GS = gs_lds == 1u ? reinterpret_cast<uint32_t*>(wsm + hcap) : gs_all + (uint64_t)blockIdx.x * ncell;
   uint8_t* GB = reinterpret_cast<uint8_t*>(wsm + hcap);
+  // free-cell bitmap after the heap and the LDS g_scores (wave_lds_bytes' carve)
+  const uint32_t gsb = gs_lds == 1u ? ncell * 4u : gs_lds == 2u ? (ncell + 15u) / 16u * 16u : 0u;
+  uint32_t* FB = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wsm + hcap) + gsb);
+  const uint32_t nfw = G.H * G.Ww;
+  if (!serial)
+    for (uint32_t t = lane; t < nfw; t += 64u) FB[t] = G.freebits[t];
   uint32_t ep = gs_lds ? 0u : epochs[blockIdx.x];
   if (gs_lds == 1u)
     for (uint32_t c = lane; c < ncell; c += 64u) GS[c] = 0u;
@@ -712,11 +913,24 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
     __syncthreads();
     const uint32_t tag = ep % 1023u + 1u;
     ++ep;
+    const AstarQuery q = Q[qi];
+    int32_t L = 0;
+    uint8_t code = NH_UNKNOWN;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t pops = 0;
+    if (!serial) {
+      code = gs_lds == 2u ? astar_wave_par<2>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, &pops)
+                          : astar_wave_par<1>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, &pops);
+    } else if (lane == 0) {
+      code = gs_lds == 2u ? astar_wave_core<2>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L)
+                          : astar_wave_core<1>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L);
+    }
+    if (prof && lane == 0) {  // TSW_ASTAR_PROF: pops, shader clocks, 100 MHz ticks per query
+      prof[3ull * qi] = pops;
+      prof[3ull * qi + 1] = __builtin_amdgcn_s_memtime() - t0;
+      prof[3ull * qi + 2] = __builtin_amdgcn_s_memrealtime() - r0;
+    }
     if (lane == 0) {
-      const AstarQuery q = Q[qi];
-      int32_t L = 0;
-      const uint8_t code = gs_lds == 2u ? astar_wave_core<2>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L)
-                                        : astar_wave_core<1>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L);
       if (L == -2) {
         ovf[atomicAdd(novf, 1u)] = q;  // heap outgrew LDS: resolved by k_astar
       } else {
@@ -836,30 +1050,67 @@ static uint32_t wave_gs_mode(const DevGrid& G) {
   return G.ncell <= WAVE_GS_LDS_MAX ? 1u : G.ncell <= WAVE_GB_LDS_MAX ? 2u : 0u;
 }
 
-static size_t wave_lds_bytes(const DevGrid& G, uint32_t hcap) {
-  const uint32_t m = wave_gs_mode(G);
-  return (size_t)hcap * 8u + (m == 1u ? (size_t)G.ncell * 4u : m == 2u ? ((size_t)G.ncell + 15u) / 16u * 16u : 0u);
+constexpr size_t WAVE_LDS_MAX = 160u * 1024u;
+
+// heap + LDS g_scores + free-cell bitmap (k_astar_wave's carve)
+static size_t wave_lds_bytes(const DevGrid& G, uint32_t hcap, uint32_t m) {
+  return (size_t)hcap * 8u + (m == 1u ? (size_t)G.ncell * 4u : m == 2u ? ((size_t)G.ncell + 15u) / 16u * 16u : 0u) +
+         (size_t)G.H * G.Ww * 4u;
 }
 
-uint32_t astar_wave_slots(const DevGrid& G, int num_cu) {
-  const size_t lds = wave_lds_bytes(G, WAVE_HCAP);
+// largest heap (<= want) whose carve fits the 160 KiB of LDS
+static uint32_t wave_fit_hcap(const DevGrid& G, uint32_t want, uint32_t m) {
+  const size_t rest = wave_lds_bytes(G, 0, m);
+  const size_t room = rest < WAVE_LDS_MAX ? (WAVE_LDS_MAX - rest) / 8u : 0u;
+  return (uint32_t)std::min<size_t>(want, room);
+}
+
+bool astar_wave_lds_gs(const DevGrid& G) { return wave_gs_mode(G) != 0u; }
+
+uint32_t astar_wave_slots(const DevGrid& G, int num_cu, bool global_gs) {
+  const uint32_t m = global_gs ? 0u : wave_gs_mode(G);
+  const size_t lds = wave_lds_bytes(G, wave_fit_hcap(G, WAVE_HCAP, m), m);
   const uint32_t per_cu = (uint32_t)std::max<size_t>(1, (160u * 1024u) / lds);
   return (uint32_t)num_cu * std::min<uint32_t>(per_cu, 16u);
 }
 
 hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
                              uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
-                             AstarQuery* ovf, uint32_t* novf, uint32_t hcap, hipStream_t s) {
+                             AstarQuery* ovf, uint32_t* novf, uint32_t hcap, bool global_gs, hipStream_t s) {
   if (nq == 0) return hipSuccess;
-  const uint32_t gs_lds = wave_gs_mode(G);
+  const uint32_t gs_lds = global_gs ? 0u : wave_gs_mode(G);
   hcap = hcap ? std::max<uint32_t>(4u, std::min(hcap, WAVE_HCAP)) : WAVE_HCAP;
-  const size_t lds = wave_lds_bytes(G, hcap);
+  hcap = wave_fit_hcap(G, hcap, gs_lds);  // overflowing queries are handed on
+  if (hcap < 4u) return hipErrorInvalidValue;
+  const size_t lds = wave_lds_bytes(G, hcap, gs_lds);
   const uint32_t grid = std::min(nq, nslots);
   hipError_t e = hipFuncSetAttribute((const void*)k_astar_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
+  const uint32_t serial = getenv("TSW_ASTAR_SERIAL") ? 1u : 0u;  // A/B and tests: lone-lane core
+  unsigned long long* prof = nullptr;
+  if (getenv("TSW_ASTAR_PROF")) {
+    e = hipMalloc(&prof, (size_t)nq * 24u);
+    if (e != hipSuccess) return e;
+    hipMemsetAsync(prof, 0, (size_t)nq * 24u, s);
+  }
   hipLaunchKernelGGL(k_astar_wave, dim3(grid), dim3(64), lds, s, G, Q, nq, nh_base, nstride, res, lens, hcap,
-                     gs_lds, gs_all, epochs, ovf, novf);
-  return hipGetLastError();
+                     gs_lds, gs_all, epochs, ovf, novf, serial, prof);
+  e = hipGetLastError();
+  if (prof) {
+    std::vector<unsigned long long> h((size_t)nq * 3u);
+    hipStreamSynchronize(s);
+    hipMemcpy(h.data(), prof, h.size() * 8u, hipMemcpyDeviceToHost);
+    hipFree(prof);
+    size_t worst = 0;
+    for (size_t i = 0; i < nq; ++i)
+      if (h[3 * i + 2] > h[3 * worst + 2]) worst = i;
+    fprintf(stderr, "[k_astar_wave] nq %u gs_mode %u hcap %u | slowest: pops %llu clocks %llu real_us %.1f -> %.1f clk/pop, %.3f us/pop, %.0f MHz\n",
+            nq, gs_lds, hcap, h[3 * worst], h[3 * worst + 1], h[3 * worst + 2] / 100.0,
+            (double)h[3 * worst + 1] / std::max(1ull, h[3 * worst]),
+            h[3 * worst + 2] / 100.0 / std::max(1ull, h[3 * worst]),
+            (double)h[3 * worst + 1] / std::max(1.0, h[3 * worst + 2] / 100.0));
+  }
+  return e;
 }
 
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,

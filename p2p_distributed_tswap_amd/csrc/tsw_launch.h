@@ -79,10 +79,14 @@ hipError_t launch_astar_lds(const DevGrid& G, const AstarQuery* Q, uint32_t nq, 
 
 // One query per wave, LDS heap (grids of > 1024 cells); gs_all/epochs: nslots u32 g_score
 // arrays of ncell words (used only when the grid's g_scores do not fit LDS).
-uint32_t astar_wave_slots(const DevGrid& G, int num_cu);
+// global_gs: keep the g_scores in the global slots even when the grid's fit LDS (second tier
+// for queries whose byte-encoded g_scores overflowed).
+uint32_t astar_wave_slots(const DevGrid& G, int num_cu, bool global_gs = false);
+bool astar_wave_lds_gs(const DevGrid& G);  // k_astar_wave keeps this grid's g_scores in LDS
 hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
                              uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
-                             AstarQuery* ovf, uint32_t* novf, uint32_t hcap /*0: default*/, hipStream_t s);
+                             AstarQuery* ovf, uint32_t* novf, uint32_t hcap /*0: default*/, bool global_gs,
+                             hipStream_t s);
 
 // Batched decentralized decision (tsw_decide.hip, agent.rs:329-462).
 constexpr uint32_t DEC_ACT_MOVE = 0, DEC_ACT_GOAL_SWAP = 1, DEC_ACT_ROTATION = 2, DEC_ACT_WAIT = 3;

@@ -80,7 +80,7 @@ def test_astar_random_pairs(name, nq):
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
 
 
-@pytest.mark.parametrize("name", ["warehouse", "cave"])
+@pytest.mark.parametrize("name", ["warehouse", "cave", "serpentine"])
 def test_astar_wave_heap_overflow_handoff(monkeypatch, name):
     """k_astar_wave (grids > 1024 cells) with a tiny LDS heap (read at context creation): queries
     that outgrow it are handed to the global-heap kernel; results stay bit-exact."""
@@ -228,3 +228,30 @@ def test_step_deterministic_and_exact(name, n, seed):
         dv = np.flatnonzero(vv != rv)
         dg = np.flatnonzero(gg != rg)
         assert dv.size == 0 and dg.size == 0, f"rep {rep}: v differs at {dv[:8]}, g differs at {dg[:8]}"
+
+
+@pytest.mark.parametrize("mode", ["coop", "serial", "no_tier2"])
+def test_astar_wave_cores_and_tiers(monkeypatch, mode):
+    """k_astar_wave's wave-cooperative heap (default), the lone-lane core (TSW_ASTAR_SERIAL) and
+    the hand-off chain byte-g LDS -> u32-g global slots (tier 2) -> k_astar, or straight to
+    k_astar (TSW_ASTAR_NO_TIER2): all bit-exact on long detour queries of the serpentine map."""
+    if mode == "serial":
+        monkeypatch.setenv("TSW_ASTAR_SERIAL", "1")
+    if mode == "no_tier2":
+        monkeypatch.setenv("TSW_ASTAR_NO_TIER2", "1")
+    rows = _grid("serpentine")
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    W = cells.shape[1]
+    free = np.flatnonzero(cells.reshape(-1) != ord("@"))
+    rng = np.random.default_rng(9)
+    # far-apart columns: the path snakes through many wall gaps (detour >> 62)
+    left = free[(free % W) < 20]
+    right = free[(free % W) > W - 20]
+    s = np.concatenate([rng.choice(left, 48), rng.choice(free, 16)]).astype(np.uint32)
+    g = np.concatenate([rng.choice(right, 48), rng.choice(free, 16)]).astype(np.uint32)
+    with Planner(rows) as p:
+        nxt, ln = p.get_path_next(s, g)
+    for q in range(s.size):
+        rn, rl, _ = og.get_path_next(int(s[q]), int(g[q]))
+        assert (nxt[q], ln[q]) == (rn, rl), f"query {s[q]}->{g[q]} ({mode})"
