@@ -708,40 +708,41 @@ __device__ __forceinline__ void wave_order() {
   asm volatile("" ::: "memory");
 }
 
-// BinaryHeap::sift_up(0, pos) with `elem` in the hole; wave-uniform arguments.
+__device__ __forceinline__ uint64_t ballot64(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
+// BinaryHeap::sift_up(0, pos) with `elem` in the hole; wave-uniform arguments. Straight-line:
+// every lane reads (lanes >= the hole's depth re-read the hole), one ballot, one store.
 __device__ __forceinline__ void wsift_up(uint64_t* Hp, uint32_t pos, uint64_t elem, uint32_t lane) {
-  const uint32_t dp = 31u - (uint32_t)__builtin_clz(pos + 1u);  // depth of the hole (root = 0)
+  const uint32_t p1 = pos + 1u;
+  const uint32_t dp = 31u - (uint32_t)__builtin_clz(p1);  // depth of the hole (root = 0)
   const uint32_t k = hk(elem);
-  uint64_t a = 0;
-  bool gt = false;
-  if (lane < dp) {
-    a = Hp[((pos + 1u) >> (dp - lane)) - 1u];  // ancestor at depth `lane`
-    gt = k < hk(a);                             // elem moves past it
-  }
-  const uint32_t t = dp - (uint32_t)__popcll(__ballot(gt));  // landing depth
+  const uint32_t sh = dp > lane ? dp - lane : 0u;
+  const uint64_t a = Hp[(p1 >> sh) - 1u];  // ancestor at depth `lane`
+  const uint64_t G = ballot64(k < hk(a)) & ((1ull << dp) - 1ull);  // ancestors elem moves past
+  const uint32_t t = dp - (uint32_t)__popcll(G);                   // landing depth
+  const bool isdp = lane == dp;
+  // lanes t..dp-1 move their ancestor one level down the path; lane dp stores elem at depth t
+  const uint32_t dst = isdp ? (p1 >> (dp - t)) - 1u : (p1 >> (sh - 1u)) - 1u;
   wave_order();
-  if (lane >= t && lane < dp) Hp[((pos + 1u) >> (dp - lane - 1u)) - 1u] = a;  // one level down the path
-  else if (lane == dp) Hp[((pos + 1u) >> (dp - t)) - 1u] = elem;
+  if (lane >= t && lane <= dp) Hp[dst] = isdp ? elem : a;
   wave_order();
 }
 
 // BinaryHeap::pop (swap last into the root, sift_down_to_bottom(0), sift_up(0, hole)); len >= 1.
+// Window lanes: lane j < 62 <-> depth kk = log2(j + 2) (1..5), index ki = j + 2 - 2^kk below the
+// hole; the first window's lanes 62 / 63 fetch the last element / the root.
 __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t lane) {
+  constexpr uint64_t M62 = (1ull << 62) - 1ull, EVEN = 0x5555555555555555ull;
   const uint32_t end = --len;
   uint32_t pos = 0;
   uint64_t last = 0, top = 0;
-  const uint32_t kk = 31u - (uint32_t)__builtin_clz(lane + 2u);  // window depth of this lane (lane < 62)
+  const uint32_t kk = 31u - (uint32_t)__builtin_clz(lane + 2u);
   const uint32_t ki = lane + 2u - (1u << kk);
   for (bool first = true;; first = false) {
-    uint32_t node = 0;
-    bool valid = false;
-    if (lane < 62u) {
-      node = ((pos + 1u) << kk) - 1u + ki;
-      valid = node < end;
-    }
-    uint64_t val = 0;
-    if (valid) val = Hp[node];
-    else if (first && lane >= 62u) val = Hp[lane == 62u ? end : 0u];
+    const uint32_t node = ((pos + 1u) << kk) - 1u + ki;
+    uint32_t addr = node < end ? node : end;  // Hp[end] is still allocated
+    if (first) addr = lane == 62u ? end : (lane == 63u ? 0u : addr);
+    const uint64_t val = Hp[addr];
     if (first) {
       last = rl64(val, 62);
       top = rl64(val, 63);
@@ -749,22 +750,21 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
     }
     const uint32_t key = hk(val);
     const uint32_t sib = (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    const uint64_t VL = __ballot(valid);
-    const uint64_t CR = __ballot(valid && !(lane & 1u) && node + 1u < end && key >= sib);
-    uint32_t idx = 0, d = 0;
-    uint64_t on = 0;
+    const uint64_t VL = ballot64(node < end) & M62;
+    // left child lane (even) takes the right child when left <= right and the right exists
+    const uint64_t CR = ballot64(key >= sib) & (VL >> 1) & EVEN;
+    uint32_t idx = 0, d = 0, live = 1;
 #pragma unroll
-    for (uint32_t k = 1; k <= 5; ++k) {
-      const uint32_t ll = (1u << k) - 2u + 2u * idx;  // lane of the left child
-      if (!((VL >> ll) & 1ull)) break;
-      const uint32_t b = (uint32_t)((CR >> ll) & 1ull);
-      idx = 2u * idx + b;
-      on |= 1ull << (ll + b);
-      d = k;
+    for (uint32_t k = 1; k <= 5; ++k) {  // branch-free SALU walk down the path
+      const uint32_t ll = (1u << k) - 2u + 2u * idx;
+      live &= (uint32_t)(VL >> ll) & 1u;
+      idx = live ? 2u * idx + ((uint32_t)(CR >> ll) & 1u) : idx;
+      d += live;
     }
     if (d == 0) break;
+    const bool on = kk <= d && ki == (idx >> (d - kk));
     wave_order();
-    if ((on >> lane) & 1ull) Hp[(node - 1u) >> 1] = val;  // move up into the parent
+    if (on) Hp[(node - 1u) >> 1] = val;  // move up into the parent
     wave_order();
     pos = ((pos + 1u) << d) - 1u + idx;
     if (d < 5) break;
@@ -774,13 +774,30 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
 }
 
 // FB: the grid's free-cell row bitmap (DevGrid::freebits) staged in LDS, so relaxing a node
-// needs no global load (a dependent L2 round trip per pop was the kernel's critical path).
-template <int GSM>
+// needs no global load.
+// PROF: pr[0..4] = pops, clocks in pops, in relaxations, in pushes, pushes (TSW_ASTAR_PROF)
+template <int GSM, bool PROF>
 __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag,
                                                   uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
-                                                  const uint32_t* FB, int32_t* len_out, uint32_t* pops_out) {
+                                                  const uint32_t* FB, int32_t* len_out, unsigned long long* pr) {
   const uint32_t lane = threadIdx.x & 63u;
-  uint32_t pops = 0;
+  unsigned long long pops = 0, c_pop = 0, c_nb = 0, c_push = 0, npush = 0, tk = 0;
+  auto tick = [&](unsigned long long& acc) {
+    if constexpr (PROF) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc += t - tk;
+      tk = t;
+    }
+  };
+  auto flush = [&]() {
+    if constexpr (PROF) {
+      pr[0] = pops;
+      pr[1] = c_pop;
+      pr[2] = c_nb;
+      pr[3] = c_push;
+      pr[4] = npush;
+    }
+  };
   const uint32_t W = G.W, H = G.H, Ww = G.Ww;
   const uint32_t vy = v / W, vx = v - vy * W, gy = goal / W, gx = goal - gy * W;
   if (v == goal) {
@@ -799,63 +816,67 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     Hp[0] = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
   }
   wave_order();
+  if constexpr (PROF) tk = __builtin_amdgcn_s_memtime();
   uint32_t len = 1;
   // lanes 0..3 own the neighbour in direction `lane` (S, E, N, W: tswap.rs:62-73)
   const uint32_t dd = lane & 3u;
   while (len > 0) {
     ++pops;
-    *pops_out = pops;
     const uint64_t e = wpop(Hp, len, lane);
+    tick(c_pop);
     const uint32_t cx = (uint32_t)(e >> 16) & 0xFFFFu, cy = (uint32_t)e & 0xFFFFu;
     const uint32_t cg = hk(e) & 0x7FFFu;
     const uint32_t c = cy * W + cx;
     if (c == goal) {
+      flush();
       *len_out = (int32_t)cg + 1;
       if constexpr (GSM == 2) return (uint8_t)((GB[goal] >> 5) & 3u);
       else return (uint8_t)((GS[goal] >> 20) & 3u);
     }
-    uint32_t labc;
-    if constexpr (GSM == 2) labc = (GB[c] >> 5) & 3u;
-    else labc = (GS[c] >> 20) & 3u;
-    const uint32_t tg = cg + 1u;
-    bool imp = false, ovf = false;
-    uint64_t ent = 0;
-    // neighbour of lane dd (unsigned wrap: x - 1 at x = 0 fails the bound test)
+    // neighbour of lane dd (unsigned wrap: x - 1 at x = 0 fails the bound test); every lane
+    // reads (out-of-grid lanes re-read the popped cell), the LDS reads issue together
     const uint32_t nx = dd == 1 ? cx + 1 : (dd == 3 ? cx - 1 : cx);
     const uint32_t ny = dd == 0 ? cy + 1 : (dd == 2 ? cy - 1 : cy);
-    const uint32_t nc = ny * W + nx;
-    uint32_t fw = 0, old = 0;
-    if (lane < 4u && nx < W && ny < H) {  // both LDS reads issue together
-      fw = FB[ny * Ww + (nx >> 5)];
-      if constexpr (GSM == 2) old = GB[nc];
-      else old = GS[nc];
+    const bool inb = lane < 4u && nx < W && ny < H;
+    const uint32_t fx = inb ? nx : cx, fy = inb ? ny : cy;
+    const uint32_t nc = fy * W + fx;
+    const uint32_t fw = FB[fy * Ww + (fx >> 5)];
+    uint32_t old, labc;
+    if constexpr (GSM == 2) {
+      old = GB[nc];
+      labc = (GB[c] >> 5) & 3u;
+    } else {
+      old = GS[nc];
+      labc = (GS[c] >> 20) & 3u;
     }
-    if ((fw >> (nx & 31u)) & 1u) {
-      uint32_t oldg, man = 0;
+    const uint32_t tg = cg + 1u;
+    uint32_t oldg, man = 0;
+    if constexpr (GSM == 2) {
+      man = (fx > vx ? fx - vx : vx - fx) + (fy > vy ? fy - vy : vy - fy);
+      oldg = (old & 0x80u) ? man + 2u * (old & 31u) : 0xFFFFFFFFu;
+    } else {
+      oldg = ((old & 0xFFC00000u) == tagw) ? (old & GS_G_MASK) : 0xFFFFFFFFu;
+    }
+    const bool imp = inb && ((fw >> (fx & 31u)) & 1u) && tg < oldg;
+    uint64_t ent = 0;
+    bool ovf = false;
+    if (imp) {
+      const uint32_t lab = cg == 0 ? dd : labc;
+      const uint32_t h = (fx > gx ? fx - gx : gx - fx) + (fy > gy ? fy - gy : gy - fy);
+      const uint32_t f = tg + h;
+      ovf = tg >= (1u << 15) || f >= (1u << 17);
       if constexpr (GSM == 2) {
-        man = (nx > vx ? nx - vx : vx - nx) + (ny > vy ? ny - vy : vy - ny);
-        oldg = (old & 0x80u) ? man + 2u * (old & 31u) : 0xFFFFFFFFu;
+        const uint32_t hh = (tg - man) >> 1;
+        ovf = ovf || hh > 31u;
+        if (!ovf) GB[nc] = (uint8_t)(0x80u | (lab << 5) | hh);
       } else {
-        oldg = ((old & 0xFFC00000u) == tagw) ? (old & GS_G_MASK) : 0xFFFFFFFFu;
+        if (!ovf) GS[nc] = tagw | (lab << 20) | tg;
       }
-      if (tg < oldg) {
-        imp = true;
-        const uint32_t lab = cg == 0 ? dd : labc;
-        const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
-        const uint32_t f = tg + h;
-        ovf = tg >= (1u << 15) || f >= (1u << 17);
-        if constexpr (GSM == 2) {
-          const uint32_t hh = (tg - man) >> 1;
-          ovf = ovf || hh > 31u;
-          if (!ovf) GB[nc] = (uint8_t)(0x80u | (lab << 5) | hh);
-        } else {
-          if (!ovf) GS[nc] = tagw | (lab << 20) | tg;
-        }
-        ent = ((uint64_t)((f << 15) | tg) << 32) | (nx << 16) | ny;
-      }
+      ent = ((uint64_t)((f << 15) | tg) << 32) | (fx << 16) | fy;
     }
-    uint64_t M = __ballot(imp);
-    if (__ballot(ovf) != 0ull || len + (uint32_t)__popcll(M) > hcap) {
+    uint64_t M = ballot64(imp);
+    tick(c_nb);
+    if (ballot64(ovf) != 0ull || len + (uint32_t)__popcll(M) > hcap) {
       *len_out = -2;
       return NH_UNKNOWN;
     }
@@ -865,8 +886,11 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       M &= M - 1ull;
       wsift_up(Hp, len, rl64(ent, d), lane);
       ++len;
+      ++npush;
     }
+    tick(c_push);
   }
+  flush();
   *len_out = 2;
   return fallback_code(G.nbmask[v], vx, vy, gx, gy);
 }
@@ -917,18 +941,22 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
     int32_t L = 0;
     uint8_t code = NH_UNKNOWN;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t pops = 0;
-    if (!serial) {
-      code = gs_lds == 2u ? astar_wave_par<2>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, &pops)
-                          : astar_wave_par<1>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, &pops);
+    unsigned long long pr[5] = {0, 0, 0, 0, 0};
+    if (!serial && prof) {
+      code = gs_lds == 2u ? astar_wave_par<2, true>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr)
+                          : astar_wave_par<1, true>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr);
+    } else if (!serial) {
+      code = gs_lds == 2u ? astar_wave_par<2, false>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr)
+                          : astar_wave_par<1, false>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr);
     } else if (lane == 0) {
       code = gs_lds == 2u ? astar_wave_core<2>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L)
                           : astar_wave_core<1>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L);
     }
     if (prof && lane == 0) {  // TSW_ASTAR_PROF: pops, shader clocks, 100 MHz ticks per query
-      prof[3ull * qi] = pops;
-      prof[3ull * qi + 1] = __builtin_amdgcn_s_memtime() - t0;
-      prof[3ull * qi + 2] = __builtin_amdgcn_s_memrealtime() - r0;
+      prof[8ull * qi + 1] = __builtin_amdgcn_s_memtime() - t0;
+      prof[8ull * qi + 2] = __builtin_amdgcn_s_memrealtime() - r0;
+      prof[8ull * qi] = pr[0];
+      for (int j = 1; j < 5; ++j) prof[8ull * qi + 2 + j] = pr[j];
     }
     if (lane == 0) {
       if (L == -2) {
@@ -1089,26 +1117,28 @@ hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq,
   const uint32_t serial = getenv("TSW_ASTAR_SERIAL") ? 1u : 0u;  // A/B and tests: lone-lane core
   unsigned long long* prof = nullptr;
   if (getenv("TSW_ASTAR_PROF")) {
-    e = hipMalloc(&prof, (size_t)nq * 24u);
+    e = hipMalloc(&prof, (size_t)nq * 64u);
     if (e != hipSuccess) return e;
-    hipMemsetAsync(prof, 0, (size_t)nq * 24u, s);
+    hipMemsetAsync(prof, 0, (size_t)nq * 64u, s);
   }
   hipLaunchKernelGGL(k_astar_wave, dim3(grid), dim3(64), lds, s, G, Q, nq, nh_base, nstride, res, lens, hcap,
                      gs_lds, gs_all, epochs, ovf, novf, serial, prof);
   e = hipGetLastError();
   if (prof) {
-    std::vector<unsigned long long> h((size_t)nq * 3u);
+    std::vector<unsigned long long> h((size_t)nq * 8u);
     hipStreamSynchronize(s);
     hipMemcpy(h.data(), prof, h.size() * 8u, hipMemcpyDeviceToHost);
     hipFree(prof);
     size_t worst = 0;
     for (size_t i = 0; i < nq; ++i)
-      if (h[3 * i + 2] > h[3 * worst + 2]) worst = i;
-    fprintf(stderr, "[k_astar_wave] nq %u gs_mode %u hcap %u | slowest: pops %llu clocks %llu real_us %.1f -> %.1f clk/pop, %.3f us/pop, %.0f MHz\n",
-            nq, gs_lds, hcap, h[3 * worst], h[3 * worst + 1], h[3 * worst + 2] / 100.0,
-            (double)h[3 * worst + 1] / std::max(1ull, h[3 * worst]),
-            h[3 * worst + 2] / 100.0 / std::max(1ull, h[3 * worst]),
-            (double)h[3 * worst + 1] / std::max(1.0, h[3 * worst + 2] / 100.0));
+      if (h[8 * i + 2] > h[8 * worst + 2]) worst = i;
+    const unsigned long long* w = &h[8 * worst];
+    const double np = (double)std::max(1ull, w[0]);
+    fprintf(stderr,
+            "[k_astar_wave] nq %u gs_mode %u hcap %u | slowest: pops %llu clocks %llu real_us %.1f -> %.1f clk/pop "
+            "(pop %.0f, relax %.0f, push %.0f; %.2f pushes/pop), %.3f us/pop, %.0f MHz\n",
+            nq, gs_lds, hcap, w[0], w[1], w[2] / 100.0, w[1] / np, w[3] / np, w[4] / np, w[5] / np, w[6] / np,
+            w[2] / 100.0 / np, (double)w[1] / std::max(1.0, w[2] / 100.0));
   }
   return e;
 }
