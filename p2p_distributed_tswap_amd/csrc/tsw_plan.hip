@@ -531,83 +531,121 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       rules_init(P, S);
       if (P.prefetch) rules_prefetch(P, S, &s_q);
       PLAN_TICK(15);
-      for (;;) {
-        const uint32_t cursor = s_ctl.i;
-        uint32_t best = NO_AGENT;
-        for (uint32_t k = cursor + tid; k < n; k += bd) {
-          const uint32_t s = S.SUCC[k];
-          if (s == SUCC_TERM || s == k) continue;
-          if (S.V[s] == S.G[s] || S.ONC[k]) {
-            best = k;  // later k of this thread are larger
-            break;
-          }
-        }
-        best = wave_min_u32(best);
-        if (lane == 0) s_wcount[wid] = best;
-        __syncthreads();
-        PLAN_TICK(13);
-        if (tid == 0) {
-          uint32_t b = NO_AGENT;
-          for (uint32_t w = 0; w < nwaves; ++w) b = s_wcount[w] < b ? s_wcount[w] : b;
-          s_best = b;
-          s_miss = 0;
-          if (b != NO_AGENT) {
-            const uint32_t s = S.SUCC[b];
-            if (S.V[s] == S.G[s]) {  // rule 3: goal swap (tswap.rs:198-202)
-              uint32_t code = S.CANDC[b];
-              if (code > NH_STAY && S.GT[b] >= 0) code = P.nh[(uint64_t)S.GT[b] * P.nstride + S.V[s]];
-              const uint32_t gb = S.G[b];
-              const int32_t tb = S.GT[b];
-              S.G[b] = S.G[s];
-              S.GT[b] = S.GT[s];
-              S.G[s] = gb;
-              S.GT[s] = tb;
-              S.CANDC[s] = NHC_DIRTY;
-              if (S.V[b] == S.G[b]) S.SUCC[b] = SUCC_TERM;  // shared start cell: b now at its goal
-              if (code <= NH_STAY) {
-                S.NHC[s] = (uint8_t)code;
-                const uint32_t ns = succ_of(P, S, s);
-                S.SUCC[s] = ns;
-                if (ns != SUCC_TERM && ns != s) {
-                  // new cycle through s?
-                  uint32_t x = ns;
-                  for (uint32_t it = 0; it < n && x != SUCC_TERM && x != s; ++it) x = S.SUCC[x];
-                  if (x == s) {
-                    uint32_t y = s;
-                    do {
-                      S.ONC[y] = 1;
-                      y = S.SUCC[y];
-                    } while (y != s);
-                  }
-                }
-              } else {
-                S.NHC[s] = NHC_DIRTY;  // unresolved: refresh + full relabel below
-                s_miss = 1;
+      // One firing agent per round (tswap.rs:180-252 in agent order): fire(b) applies b's rule 3
+      // swap or rule 4 rotation (tid 0 only) and sets s_miss when next hops must be refreshed.
+      auto fire = [&](uint32_t b) {
+        const uint32_t s = S.SUCC[b];
+        if (S.V[s] == S.G[s]) {  // rule 3: goal swap (tswap.rs:198-202)
+          uint32_t code = S.CANDC[b];
+          if (code > NH_STAY && S.GT[b] >= 0) code = P.nh[(uint64_t)S.GT[b] * P.nstride + S.V[s]];
+          const uint32_t gb = S.G[b];
+          const int32_t tb = S.GT[b];
+          S.G[b] = S.G[s];
+          S.GT[b] = S.GT[s];
+          S.G[s] = gb;
+          S.GT[s] = tb;
+          S.CANDC[s] = NHC_DIRTY;
+          if (S.V[b] == S.G[b]) S.SUCC[b] = SUCC_TERM;  // shared start cell: b now at its goal
+          if (code <= NH_STAY) {
+            S.NHC[s] = (uint8_t)code;
+            const uint32_t ns = succ_of(P, S, s);
+            S.SUCC[s] = ns;
+            if (ns != SUCC_TERM && ns != s) {
+              // new cycle through s?
+              uint32_t x = ns;
+              for (uint32_t it = 0; it < n && x != SUCC_TERM && x != s; ++it) x = S.SUCC[x];
+              if (x == s) {
+                uint32_t y = s;
+                do {
+                  S.ONC[y] = 1;
+                  y = S.SUCC[y];
+                } while (y != s);
               }
-            } else {  // rule 4: rotate targets along the cycle b -> s -> ... -> last -> b
-              uint32_t L = 0;
-              // cycle members in S.F2 (free until the rules_init this rotation triggers; LDS when
-              // the agent arrays are): the walk below re-reads them serially
-              uint32_t* ap = S.F2;
-              for (uint32_t a = b; L == 0 || a != b; a = S.SUCC[a]) ap[L++] = a;
-              const uint32_t last = ap[L - 1];
-              const uint32_t last_goal = S.G[last];
-              const int32_t last_tab = S.GT[last];
-              for (uint32_t kk = L - 1; kk >= 1; --kk) {
-                const uint32_t a = ap[kk], pa = ap[kk - 1];
-                S.G[a] = S.G[pa];
-                S.GT[a] = S.GT[pa];
-                S.NHC[a] = NHC_DIRTY;
-              }
-              S.G[b] = last_goal;
-              S.GT[b] = last_tab;
-              S.NHC[b] = NHC_DIRTY;
-              s_miss = 1;  // members' next hops changed: refresh + full relabel below
             }
-            s_ctl.i = b + 1;
-            s_ctl.rule_rounds += 1;
           } else {
-            s_ctl.i = n;
+            S.NHC[s] = NHC_DIRTY;  // unresolved: refresh + full relabel below
+            s_miss = 1;
+          }
+        } else {  // rule 4: rotate targets along the cycle b -> s -> ... -> last -> b
+          uint32_t L = 0;
+          // cycle members in S.F2 (free until the rules_init this rotation triggers; LDS when
+          // the agent arrays are): the walk below re-reads them serially
+          uint32_t* ap = S.F2;
+          for (uint32_t a = b; L == 0 || a != b; a = S.SUCC[a]) ap[L++] = a;
+          const uint32_t last = ap[L - 1];
+          const uint32_t last_goal = S.G[last];
+          const int32_t last_tab = S.GT[last];
+          for (uint32_t kk = L - 1; kk >= 1; --kk) {
+            const uint32_t a = ap[kk], pa = ap[kk - 1];
+            S.G[a] = S.G[pa];
+            S.GT[a] = S.GT[pa];
+            S.NHC[a] = NHC_DIRTY;
+          }
+          S.G[b] = last_goal;
+          S.GT[b] = last_tab;
+          S.NHC[b] = NHC_DIRTY;
+          s_miss = 1;  // members' next hops changed: refresh + full relabel below
+        }
+        s_ctl.i = b + 1;
+        s_ctl.rule_rounds += 1;
+      };
+      // n <= 512: wave 0 alone runs scan + fire rounds back to back — the scan is a ballot over
+      // 64 agents from the cursor, the fire is lane 0 of the same wave, so a round needs no
+      // workgroup barrier and no cross-wave reduction; the block joins only when a firing
+      // changed next hops (refresh + relabel) or the phase ends.
+      const bool wave_scan = n <= 512u;
+      for (;;) {
+        if (wave_scan) {
+          if (wid == 0) {
+            for (;;) {
+              __threadfence_block();
+              const uint32_t cursor = *(volatile uint32_t*)&s_ctl.i;
+              uint32_t b = NO_AGENT;
+              for (uint32_t base = cursor; base < n; base += 64u) {
+                const uint32_t k = base + lane;
+                bool f = false;
+                if (k < n) {
+                  const uint32_t s = S.SUCC[k];
+                  f = s != SUCC_TERM && s != k && (S.V[s] == S.G[s] || S.ONC[k]);
+                }
+                const uint64_t m = __ballot(f);
+                if (m) {
+                  b = base + (uint32_t)__builtin_ctzll(m);
+                  break;
+                }
+              }
+              if (lane == 0) {
+                s_best = b;
+                s_miss = 0;
+                if (b != NO_AGENT) fire(b);
+                else s_ctl.i = n;
+              }
+              __threadfence_block();
+              if (b == NO_AGENT || *(volatile uint32_t*)&s_miss) break;
+            }
+          }
+        } else {
+          const uint32_t cursor = s_ctl.i;
+          uint32_t best = NO_AGENT;
+          for (uint32_t k = cursor + tid; k < n; k += bd) {
+            const uint32_t s = S.SUCC[k];
+            if (s == SUCC_TERM || s == k) continue;
+            if (S.V[s] == S.G[s] || S.ONC[k]) {
+              best = k;  // later k of this thread are larger
+              break;
+            }
+          }
+          best = wave_min_u32(best);
+          if (lane == 0) s_wcount[wid] = best;
+          __syncthreads();
+          PLAN_TICK(13);
+          if (tid == 0) {
+            uint32_t b = NO_AGENT;
+            for (uint32_t w = 0; w < nwaves; ++w) b = s_wcount[w] < b ? s_wcount[w] : b;
+            s_best = b;
+            s_miss = 0;
+            if (b != NO_AGENT) fire(b);
+            else s_ctl.i = n;
           }
         }
         __syncthreads();
