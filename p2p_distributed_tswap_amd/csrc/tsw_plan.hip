@@ -701,6 +701,106 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         __syncthreads();
         if (tid == 0) s_ctl.i = 1;  // DEC initialised for this step (survives relaunches)
       }
+      // Round passes as per-agent bodies, run either block-wide (k = tid, tid + bd, ...) or, in
+      // the tail, by wave 0 alone over a compact list of the still-open agents.
+      uint64_t tag = 0;
+      // pass 1: target cell of an open agent; MU[c] = lowest open agent targeting c, as a
+      // round-tagged max of ~k (no reset pass: entries of older rounds are stale)
+      auto pass1 = [&](uint32_t k) -> bool {
+        if (S.DEC[k] != DEC_OPEN) return false;
+        const int code = lookup_code(P, S, k);
+        if (code < 0) {
+          if (code == -2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
+          else enqueue_pair(P, S.V[k], S.G[k], S.GT[k], &s_q);
+          s_miss = 1;
+          S.SUCC[k] = NO_CELL;
+          return true;
+        }
+        const uint32_t u = step_cell(S.V[k], (uint32_t)code, W);
+        S.SUCC[k] = u;
+        atomicMax(reinterpret_cast<unsigned long long*>(&S.MU[u]), (unsigned long long)(tag | (uint32_t)~k));
+        return true;
+      };
+      auto mu_of = [&](uint32_t c) -> uint32_t {  // lowest open agent targeting c this round
+        const uint64_t x = S.MU[c];
+        return (x >> 32) == (tag >> 32) ? ~(uint32_t)x : NO_AGENT;
+      };
+      // pass 2: tentatively decide an open agent whose turn can be replayed from the round-start
+      // state. What k reads at its turn is OCC[u] (u = its target), the occupant j's cell, goal
+      // and next hop, and its own cell; an undecided agent a < k changes one of them only by
+      // targeting u (MU[u] != k), by being the occupant (j < k still open) or by targeting k's
+      // cell (MU[v] < k). That alone is not enough: an open agent k whose open occupant b < k is
+      // its mutual-swap partner is carried to b's cell before its turn and then targets a cell
+      // nobody can name yet, so no agent above the lowest such k (s_best) may commit this
+      // round. The same pass finds it.
+      auto pass2 = [&](uint32_t k) {
+        if (S.DEC[k] != DEC_OPEN) return;
+        const uint32_t u = S.SUCC[k], v = S.V[k];
+        const uint32_t o = S.OCC[u];
+        if (o != OCC_NONE) {
+          const uint32_t b = o & OCC_IDX;
+          if (b < k && S.DEC[b] != DEC_DONE && S.SUCC[b] == v) {
+            atomicMin(&s_best, k);
+            return;
+          }
+        }
+        if (mu_of(u) != k) return;
+        if (mu_of(v) < k) return;
+        uint8_t act;
+        if (o == OCC_NONE) {
+          act = DEC_MOVE;  // rule 2
+        } else {
+          const uint32_t j = o & OCC_IDX;
+          if (j == k) {
+            act = DEC_STAY;
+          } else {
+            if (j < k && S.DEC[j] != DEC_DONE) return;  // occupant still open below k
+            if (S.V[j] == S.G[j]) {
+              act = DEC_STAY;
+            } else {
+              const int cj = lookup_code(P, S, j);
+              if (cj < 0) {
+                if (cj == -2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
+                else enqueue_pair(P, S.V[j], S.G[j], S.GT[j], &s_q);
+                s_miss = 1;
+                return;
+              }
+              act = step_cell(S.V[j], (uint32_t)cj, W) == v ? DEC_SWAP : DEC_STAY;  // :273
+            }
+          }
+        }
+        S.DEC[k] = act;
+      };
+      // pass 3: commit below s_best (disjoint cells by construction); undo the rest
+      auto pass3 = [&](uint32_t k, uint32_t spmin) {
+        const uint8_t d = S.DEC[k];
+        if (d < DEC_STAY) return;
+        if (k >= spmin) {
+          S.DEC[k] = DEC_OPEN;
+          return;
+        }
+        S.DEC[k] = DEC_DONE;
+        if (d == DEC_STAY) return;
+        const uint32_t u = S.SUCC[k], v = S.V[k];
+        if (d == DEC_MOVE) {
+          S.V[k] = u;
+          S.OCC[u] = k;
+          S.OCC[v] = OCC_NONE;
+          S.NHC[k] = NHC_DIRTY;
+        } else {
+          const uint32_t j = S.OCC[u] & OCC_IDX;
+          S.V[k] = u;
+          S.V[j] = v;
+          S.OCC[u] = k;
+          S.OCC[v] = j;
+          S.NHC[k] = NHC_DIRTY;
+          S.NHC[j] = NHC_DIRTY;
+        }
+      };
+      // Within a round DEC only goes OPEN -> {STAY, MOVE, SWAP} (own entry, pass 2) and the
+      // commit pass turns those into DONE (or back to OPEN), so "open at round start" reads
+      // as DEC != DEC_DONE for every other agent throughout the round.
+      bool tail = false;  // block-uniform: the remaining rounds run in wave 0
       for (;;) {
         if (tid == 0) {
           s_miss = 0;
@@ -709,114 +809,69 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           if (P.dbg) s_tp = wall_clock64();
         }
         __syncthreads();
-        // Within a round DEC only goes OPEN -> {STAY, MOVE, SWAP} (own entry, pass 2) and the
-        // commit pass turns those into DONE (or back to OPEN), so "open at round start" reads
-        // as DEC != DEC_DONE for every other agent throughout the round.
-        const uint64_t tag = (uint64_t)s_ctl.move_rounds << 32;
-        // pass 1: target cell of every open agent; MU[c] = lowest open agent targeting c, as
-        // a round-tagged max of ~k (no reset pass: entries of older rounds are stale)
+        tag = (uint64_t)s_ctl.move_rounds << 32;
         int open = 0;
-        for (uint32_t k = tid; k < n; k += bd) {
-          if (S.DEC[k] != DEC_OPEN) continue;
-          open = 1;
-          const int code = lookup_code(P, S, k);
-          if (code < 0) {
-            if (code == -2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
-            else enqueue_pair(P, S.V[k], S.G[k], S.GT[k], &s_q);
-            s_miss = 1;
-            S.SUCC[k] = NO_CELL;
-            continue;
-          }
-          const uint32_t u = step_cell(S.V[k], (uint32_t)code, W);
-          S.SUCC[k] = u;
-          atomicMax(reinterpret_cast<unsigned long long*>(&S.MU[u]), (unsigned long long)(tag | (uint32_t)~k));
-        }
-        open = __syncthreads_or(open);
+        for (uint32_t k = tid; k < n; k += bd) open |= pass1(k) ? 1 : 0;
+        // one agent per thread: the count is exact and decides the switch to the wave tail
+        const int nopen = n <= bd ? __syncthreads_count(open) : __syncthreads_or(open);
         PLAN_TICK(8);
-        if (!open) break;
+        if (!nopen) break;
         if (s_miss) break;  // exit to K3 below
-        auto mu_of = [&](uint32_t c) -> uint32_t {  // lowest open agent targeting c this round
-          const uint64_t x = S.MU[c];
-          return (x >> 32) == (tag >> 32) ? ~(uint32_t)x : NO_AGENT;
-        };
-        // pass 2: tentatively decide every open agent whose turn can be replayed from the
-        // round-start state. What k reads at its turn is OCC[u] (u = its target), the
-        // occupant j's cell, goal and next hop, and its own cell; an undecided agent a < k
-        // changes one of them only by targeting u (MU[u] != k), by being the occupant (j < k
-        // still open) or by targeting k's cell (MU[v] < k). That alone is not enough: an
-        // open agent k whose open occupant b < k is its mutual-swap partner is carried to
-        // b's cell before its turn and then targets a cell nobody can name yet, so no agent
-        // above the lowest such k (s_best) may commit this round. The same pass finds it.
-        for (uint32_t k = tid; k < n; k += bd) {
-          if (S.DEC[k] != DEC_OPEN) continue;
-          const uint32_t u = S.SUCC[k], v = S.V[k];
-          const uint32_t o = S.OCC[u];
-          if (o != OCC_NONE) {
-            const uint32_t b = o & OCC_IDX;
-            if (b < k && S.DEC[b] != DEC_DONE && S.SUCC[b] == v) {
-              atomicMin(&s_best, k);
-              continue;
-            }
+        if (n <= bd && nopen <= 64) {
+          // compact the open agents (index order) into `list` for the wave tail
+          const uint64_t bal = __ballot(open != 0);
+          if (lane == 0) s_wcount[wid] = (uint32_t)__popcll(bal);
+          __syncthreads();
+          if (open) {
+            uint32_t off = 0;
+            for (uint32_t w = 0; w < wid; ++w) off += s_wcount[w];
+            list[off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = tid;
           }
-          if (mu_of(u) != k) continue;
-          if (mu_of(v) < k) continue;
-          uint8_t act;
-          if (o == OCC_NONE) {
-            act = DEC_MOVE;  // rule 2
-          } else {
-            const uint32_t j = o & OCC_IDX;
-            if (j == k) {
-              act = DEC_STAY;
-            } else {
-              if (j < k && S.DEC[j] != DEC_DONE) continue;  // occupant still open below k
-              if (S.V[j] == S.G[j]) {
-                act = DEC_STAY;
-              } else {
-                const int cj = lookup_code(P, S, j);
-                if (cj < 0) {
-                  if (cj == -2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
-                  else enqueue_pair(P, S.V[j], S.G[j], S.GT[j], &s_q);
-                  s_miss = 1;
-                  continue;
-                }
-                act = step_cell(S.V[j], (uint32_t)cj, W) == v ? DEC_SWAP : DEC_STAY;  // :273
-              }
-            }
-          }
-          S.DEC[k] = act;
+          __syncthreads();
+          tail = true;
+          break;
         }
+        for (uint32_t k = tid; k < n; k += bd) pass2(k);
         __syncthreads();
         PLAN_TICK(10);
-        // pass 3: commit below s_best (disjoint cells by construction); undo the rest
         const uint32_t spmin = s_best;
-        for (uint32_t k = tid; k < n; k += bd) {
-          const uint8_t d = S.DEC[k];
-          if (d < DEC_STAY) continue;
-          if (k >= spmin) {
-            S.DEC[k] = DEC_OPEN;
-            continue;
-          }
-          S.DEC[k] = DEC_DONE;
-          if (d == DEC_STAY) continue;
-          const uint32_t u = S.SUCC[k], v = S.V[k];
-          if (d == DEC_MOVE) {
-            S.V[k] = u;
-            S.OCC[u] = k;
-            S.OCC[v] = OCC_NONE;
-            S.NHC[k] = NHC_DIRTY;
-          } else {
-            const uint32_t j = S.OCC[u] & OCC_IDX;
-            S.V[k] = u;
-            S.V[j] = v;
-            S.OCC[u] = k;
-            S.OCC[v] = j;
-            S.NHC[k] = NHC_DIRTY;
-            S.NHC[j] = NHC_DIRTY;
-          }
-        }
+        for (uint32_t k = tid; k < n; k += bd) pass3(k, spmin);
         __syncthreads();
         PLAN_TICK(12);
         if (s_miss) break;
+      }
+      if (tail) {
+        // Wave tail: <= 64 open agents, one per lane of wave 0. The round that switched has
+        // run pass 1; every pass boundary is a wave-level fence (LDS is in order per wave).
+        if (wid == 0) {
+          uint32_t nl = 0;
+          for (uint32_t w = 0; w < nwaves; ++w) nl += s_wcount[w];
+          const uint32_t k = lane < nl ? list[lane] : NO_AGENT;
+          uint32_t kk = k;
+          for (bool first = true;; first = false) {
+            if (!first) {
+              if (lane == 0) {
+                s_miss = 0;
+                s_best = NO_AGENT;
+                s_ctl.move_rounds += 1;
+              }
+              __threadfence_block();
+              tag = (uint64_t)(*(volatile uint32_t*)&s_ctl.move_rounds) << 32;
+              const bool op = kk != NO_AGENT && pass1(kk);
+              __threadfence_block();
+              if (__ballot(op) == 0ull) break;
+              if (*(volatile uint32_t*)&s_miss) break;
+            }
+            if (kk != NO_AGENT) pass2(kk);
+            __threadfence_block();
+            const uint32_t spmin = *(volatile uint32_t*)&s_best;
+            if (kk != NO_AGENT) pass3(kk, spmin);
+            __threadfence_block();
+            if (*(volatile uint32_t*)&s_miss) break;
+            if (kk != NO_AGENT && S.DEC[kk] != DEC_OPEN) kk = NO_AGENT;  // committed: leaves the tail
+          }
+        }
+        __syncthreads();
       }
       if (s_miss) {
         if (tid == 0) {
