@@ -90,6 +90,7 @@ struct tsw_ctx {
   uint32_t* d_ep16 = nullptr;
   AstarQuery* d_ovf = nullptr;
   AstarQuery* d_ovf2 = nullptr;  // second-tier overflow list (same capacity as d_ovf)
+  std::vector<uint32_t> h_lpt_goals, h_lpt_slots;  // K1 launch-order staging (bfs_lpt_order)
   size_t ovf_cap = 0;
 
   // query queue
@@ -262,6 +263,38 @@ int ensure_tmp(tsw_ctx* c, size_t k) {
   HIPCHK(dgrow(c->d_tmp_b, cb, k));
   c->tmp_cap = std::min(ca, cb);
   return TSW_OK;
+}
+
+// K1 launch order: longest BFS first. A goal's level count is its eccentricity; the distance
+// to the farthest grid corner bounds it and ranks goals well enough that the work queue's last
+// wave of goals is the short ones (LPT scheduling) instead of a few long ones running on an
+// otherwise idle chip. Output positions are carried in `slots`. TSW_BFS_ORDER=0 keeps the
+// caller's order (A/B).
+void bfs_lpt_order(const tsw_ctx* c, std::vector<uint32_t>& goals, std::vector<uint32_t>& slots) {
+  static const bool off = getenv("TSW_BFS_ORDER") && atoi(getenv("TSW_BFS_ORDER")) == 0;
+  if (off || goals.size() < 2) return;
+  const uint32_t W = c->G.W, H = c->G.H, maxe = W + H;
+  // counting sort by eccentricity bound, descending, stable: O(k + W + H) on the host
+  std::vector<uint32_t> cnt(maxe + 1u, 0u), ecc(goals.size());
+  for (size_t i = 0; i < goals.size(); ++i) {
+    const uint32_t y = goals[i] / W, x = goals[i] - y * W;
+    ecc[i] = maxe - (std::max(x, W - 1 - x) + std::max(y, H - 1 - y));
+    ++cnt[ecc[i]];
+  }
+  uint32_t acc = 0;
+  for (uint32_t e = 0; e <= maxe; ++e) {
+    const uint32_t t = cnt[e];
+    cnt[e] = acc;
+    acc += t;
+  }
+  std::vector<uint32_t> g2(goals.size()), s2(goals.size());
+  for (size_t i = 0; i < goals.size(); ++i) {
+    const uint32_t j = cnt[ecc[i]]++;
+    g2[j] = goals[i];
+    s2[j] = slots[i];
+  }
+  goals.swap(g2);
+  slots.swap(s2);
 }
 
 int ensure_astar_scratch(tsw_ctx* c) {
@@ -587,9 +620,14 @@ int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
     c->h_tab_goal[slots[k]] = newg[k];
   }
   c->tab_count = (uint32_t)need;
+  std::vector<uint32_t>& lg = c->h_lpt_goals;
+  std::vector<uint32_t>& ls = c->h_lpt_slots;
+  lg = newg;
+  ls = slots;
+  bfs_lpt_order(c, lg, ls);
   TRY(ensure_tmp(c, newg.size()));
-  HIPCHK(hipMemcpyAsync(c->d_tmp_a, newg.data(), newg.size() * 4, hipMemcpyHostToDevice, c->s));
-  HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_a, lg.data(), lg.size() * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_b, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, c->s));
   TRY(run_bfs(c, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh));
   c->st.bfs_goals += newg.size();
   c->st.bfs_launches++;
@@ -1254,8 +1292,16 @@ int tsw_dist_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16
   for (uint32_t i = 0; i < k; ++i)
     if (!cell_id_ok(c, goals[i])) RET(TSW_EINVAL, "goal cell off-grid or blocked");
   TRY(ensure_tmp(c, k));
-  HIPCHK(hipMemcpyAsync(c->d_tmp_a, goals, (size_t)k * 4, hipMemcpyHostToDevice, c->s));
-  TRY(run_bfs(c, c->d_tmp_a, nullptr, k, dev_out, c->G.ncell, nullptr));
+  // context-owned staging (like the caller's `goals`, read by the copy before it returns)
+  std::vector<uint32_t>& lg = c->h_lpt_goals;
+  std::vector<uint32_t>& ls = c->h_lpt_slots;
+  lg.assign(goals, goals + k);
+  ls.resize(k);
+  for (uint32_t i = 0; i < k; ++i) ls[i] = i;
+  bfs_lpt_order(c, lg, ls);
+  HIPCHK(hipMemcpyAsync(c->d_tmp_a, lg.data(), (size_t)k * 4, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_tmp_b, ls.data(), (size_t)k * 4, hipMemcpyHostToDevice, c->s));
+  TRY(run_bfs(c, c->d_tmp_a, c->d_tmp_b, k, dev_out, c->G.ncell, nullptr));
   c->st.bfs_goals += k;
   c->st.bfs_launches++;
   TRY(check_err(c));
