@@ -428,7 +428,6 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         rs &= rs - 1u;
       }
     };
-    // two words in flight: the decode of one overlaps the other's anchor loads
     auto decode = [&](const Word& cu) {
       const uint32_t y = cu.y, cw = cu.cw, r = cu.r, p0 = cu.p0, vis = cu.vis, wl = cu.wl, f0 = cu.f0;
       const uint32_t rsw = f0 & ~(f0 << 1);
@@ -479,13 +478,22 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
           if (b < cnt) dst[b] = (uint16_t)(pk[b >> 1] >> ((b & 1u) * 16u));
       }
     };
-    Word wa{}, wb{};
-    if (lane < nwords) fetch(lane, wa);
-    for (uint32_t k = lane; k < nwords; k += 128u) {
-      if (k + 64u < nwords) fetch(k + 64u, wb);
-      decode(wa);
-      if (k + 128u < nwords) fetch(k + 128u, wa);
-      if (k + 64u < nwords) decode(wb);
+    // four words in flight per lane (ring w0..w3, fetch distance 4): a decode waits on loads
+    // issued three decodes earlier, enough to cover L2 latency at this residency
+    Word w0{}, w1{}, w2{}, w3{};
+    if (lane < nwords) fetch(lane, w0);
+    if (lane + 64u < nwords) fetch(lane + 64u, w1);
+    if (lane + 128u < nwords) fetch(lane + 128u, w2);
+    if (lane + 192u < nwords) fetch(lane + 192u, w3);
+    for (uint32_t k = lane; k < nwords; k += 256u) {
+      decode(w0);
+      if (k + 256u < nwords) fetch(k + 256u, w0);
+      if (k + 64u < nwords) decode(w1);
+      if (k + 320u < nwords) fetch(k + 320u, w1);
+      if (k + 128u < nwords) decode(w2);
+      if (k + 384u < nwords) fetch(k + 384u, w2);
+      if (k + 192u < nwords) decode(w3);
+      if (k + 448u < nwords) fetch(k + 448u, w3);
     }
     lds_sync();  // the next goal re-initialises this wave's LDS
     if (A.prof) {
