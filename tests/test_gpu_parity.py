@@ -181,6 +181,24 @@ def test_mapd_more(name, n, m, seed, flags):
     assert np.array_equal(rec, ref)
 
 
+@pytest.mark.parametrize("n,max_t", [(600, 60), (1100, 40)])
+def test_mapd_block_paths(n, max_t):
+    """k_plan's block-wide paths: n > 512 runs the rules scan across the whole workgroup (not
+    wave 0 alone), n > 1024 (block < n) never enters the movement wave tail. A capped horizon
+    keeps the oracle fast; records and goals bit-exact."""
+    rows = _grid("warehouse")
+    starts, tasks = maps.make_instance(rows, n, 3 * n, 0x5EED + n)
+    og = OracleGraph(maps.rows_to_array(rows))
+    ref, rgoal = og.mapd(starts, tasks, max_t, trace_goals=True)
+    with Planner(rows) as p:
+        rec, goal = p.plan_mapd_arrays(starts, tasks, max_t, trace_goals=True)
+    assert rec.shape == ref.shape
+    if not np.array_equal(goal, rgoal):
+        t = int(np.argmax((goal != rgoal).any(axis=0)))
+        pytest.fail(f"goal divergence first at t={t}")
+    assert np.array_equal(rec, ref)
+
+
 @pytest.mark.parametrize("name,flags,ngoals", [("rand32", TSW_F_EAGER_NEXTHOP, 0), ("rand16", TSW_F_EAGER_NEXTHOP, 0),
                                                ("open8", TSW_F_EAGER_NEXTHOP, 0)])
 def test_next_hop_tables_all_pairs(name, flags, ngoals):
