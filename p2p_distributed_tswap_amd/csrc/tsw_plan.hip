@@ -244,6 +244,22 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
   __syncthreads();
 }
 
+// Parallel: the next hop of every agent from the cell its resolved code points at (the pair the
+// movement phase or the next step reads after the agent moves, tswap.rs:263-273); speculative,
+// bounded by half the queue like rules_prefetch.
+__device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  for (uint32_t k = tid; k < P.n; k += bd) {
+    if (*(volatile uint32_t*)s_q >= P.qcap / 2u) break;
+    const int32_t tab = S.GT[k];
+    const uint8_t c = S.NHC[k];
+    if (tab < 0 || c >= NH_STAY || S.V[k] == S.G[k]) continue;
+    const uint32_t u = step_cell(S.V[k], c, P.W);
+    if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) enqueue_pair(P, u, S.G[k], tab, s_q);
+  }
+  __syncthreads();
+}
+
 // Serial movement phase (tswap.rs:257-285) — used when cells are shared by several agents
 // (duplicate start cells); false on an unresolved next hop.
 __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
@@ -505,6 +521,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       __syncthreads();
     } else if (sec == SEC_PRE1 || sec == SEC_PRE2) {
       const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
+      // step start: queue every agent's next hop from the cell it is about to enter now, so
+      // the assignment exit's K3 batch (if any) already carries what the movement phase reads
+      if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, &s_q);
       if (q > 0) {
         if (tid == 0) {
           s_ctl.qcount = s_q;
