@@ -697,6 +697,9 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.has_dups = *c->h_dups;
   // speculative next-hop prefetch only pays in lazy mode (eager tables have nothing unresolved)
   P.prefetch = (getenv("TSW_NO_PREFETCH") || eager_policy(c, 0)) ? 0u : 1u;
+  // wide prefetch (default 4 hops): every agent's (succ cell, goal) pair, and its path walked this
+  // many hops ahead; TSW_WIDE_PREFETCH=0 restores candidates-only / one hop (A/B)
+  P.wide_prefetch = getenv("TSW_WIDE_PREFETCH") ? (uint32_t)std::max(0, atoi(getenv("TSW_WIDE_PREFETCH"))) : 4u;
   P.pick_xy = c->d_pick_xy;
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;

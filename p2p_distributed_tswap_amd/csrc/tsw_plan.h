@@ -44,6 +44,7 @@ struct PlanArgs {
   uint32_t n, m, W, ncell;
   uint32_t mode, agents_lds, occ_lds, tasks_lds;
   uint32_t has_dups, prefetch;  // prefetch: enqueue rules-round next hops up front (rules_prefetch)
+  uint32_t wide_prefetch;       // 0: off; else also (succ cell, goal) of every agent, path walked this many hops ahead
   uint32_t* v;
   uint32_t* g;
   uint8_t* st;

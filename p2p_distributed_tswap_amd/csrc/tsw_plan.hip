@@ -237,7 +237,7 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
     }
     const uint32_t s = S.SUCC[k];
     if (s == SUCC_TERM || s == k) continue;
-    if (!(S.ONC[k] || S.V[s] == S.G[s])) continue;
+    if (!P.wide_prefetch && !(S.ONC[k] || S.V[s] == S.G[s])) continue;
     const uint32_t vs = S.V[s];
     if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) enqueue_pair(P, vs, S.G[k], tab, s_q);
   }
@@ -248,14 +248,23 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
 // movement phase or the next step reads after the agent moves, tswap.rs:263-273); speculative,
 // bounded by half the queue like rules_prefetch.
 __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
-  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  const uint32_t tid = threadIdx.x, bd = blockDim.x, hops = P.wide_prefetch ? P.wide_prefetch : 1u;
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (*(volatile uint32_t*)s_q >= P.qcap / 2u) break;
     const int32_t tab = S.GT[k];
     const uint8_t c = S.NHC[k];
     if (tab < 0 || c >= NH_STAY || S.V[k] == S.G[k]) continue;
-    const uint32_t u = step_cell(S.V[k], c, P.W);
-    if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) enqueue_pair(P, u, S.G[k], tab, s_q);
+    // walk the resolved codes up to `hops` cells ahead; queue the first unresolved one
+    uint32_t u = step_cell(S.V[k], c, P.W);
+    for (uint32_t h = 0; h < hops && u != S.G[k]; ++h) {
+      const uint8_t cu = P.nh[(uint64_t)tab * P.nstride + u];
+      if (cu == NH_UNKNOWN) {
+        enqueue_pair(P, u, S.G[k], tab, s_q);
+        break;
+      }
+      if (cu >= NH_STAY) break;  // pending, or a stay code
+      u = step_cell(u, cu, P.W);
+    }
   }
   __syncthreads();
 }
