@@ -699,6 +699,10 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.prefetch = (getenv("TSW_NO_PREFETCH") || eager_policy(c, 0)) ? 0u : 1u;
   // wide prefetch (default 4 hops): every agent's (succ cell, goal) pair, and its path walked this
   // many hops ahead; TSW_WIDE_PREFETCH=0 restores candidates-only / one hop (A/B)
+  // wave-0 rules rounds (scan 64 agents per ballot from the cursor, fire in lane 0): firing
+  // agents are dense, so a scan rarely needs more than a chunk or two even for 10k agents;
+  // TSW_WAVE_RULES_MAX caps n for A/B
+  P.wave_rules_max = getenv("TSW_WAVE_RULES_MAX") ? (uint32_t)std::max(0, atoi(getenv("TSW_WAVE_RULES_MAX"))) : 0xFFFFFFFFu;
   P.wide_prefetch = getenv("TSW_WIDE_PREFETCH") ? (uint32_t)std::max(0, atoi(getenv("TSW_WIDE_PREFETCH"))) : 4u;
   P.pick_xy = c->d_pick_xy;
   P.pick = c->d_pick;
@@ -717,8 +721,11 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   // LDS residency, in priority order: agents, occupancy grid, task table
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
-  bool oc = plan_lds_bytes(n, P.ncell, m, ag, true, false) <= budget;
-  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true) <= budget;
+  // without the agent arrays, the rules relabel's pointer-doubling buffers come next
+  bool fl = !ag && !getenv("TSW_NO_FLINKS_LDS") && plan_lds_bytes(n, P.ncell, m, false, false, false, true) <= budget;
+  bool oc = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl) <= budget;
+  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl) <= budget;
+  P.f_lds = fl;
   P.agents_lds = ag;
   P.occ_lds = oc;
   P.tasks_lds = tk;
@@ -738,7 +745,7 @@ int build_occ(tsw_ctx* c, uint32_t n) {
 int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   *c->h_ctl = init;
   HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
-  const size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds);
+  const size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds);
   // one lane per agent in the parallel passes when possible; >= 4 waves for the task argmin
   uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
   if (const char* e = getenv("TSW_PLAN_BLOCK")) block = (uint32_t)std::max(64, std::min(atoi(e), 1024)) / 64u * 64u;

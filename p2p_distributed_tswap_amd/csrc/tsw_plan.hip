@@ -43,6 +43,7 @@ constexpr uint32_t OCC_IDX = 0x7FFFFFFFu;
 constexpr uint32_t SUCC_TERM = 0xFFFFFFFFu;
 constexpr uint32_t NO_AGENT = 0xFFFFFFFFu;
 constexpr uint32_t NO_CELL = 0xFFFFFFFFu;
+constexpr uint32_t LIST_CAP = 1024;  // entries of the kernel's LDS `list` (ASSIGN compaction, changed agents)
 // movement-round decision states
 constexpr uint8_t DEC_OPEN = 0, DEC_DONE = 1, DEC_STAY = 2, DEC_MOVE = 3, DEC_SWAP = 4;
 
@@ -244,6 +245,30 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
   __syncthreads();
 }
 
+// rules_prefetch restricted to the agents a firing changed (rule 3: b and s, rule 4: the cycle):
+// only their goals, hence their next hops and successors, moved, so only their pairs are new.
+// After rules_init (SUCC valid).
+__device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t* s_q, const uint32_t* lst,
+                                    uint32_t cnt) {
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  for (uint32_t i = tid; i < cnt; i += bd) {
+    if (*(volatile uint32_t*)s_q >= P.qcap / 2u) break;
+    const uint32_t k = lst[i];
+    const int32_t tab = S.GT[k];
+    if (tab < 0) continue;
+    const uint8_t c = S.NHC[k];
+    if (c < NH_STAY && S.V[k] != S.G[k]) {
+      const uint32_t u = step_cell(S.V[k], c, P.W);
+      if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) enqueue_pair(P, u, S.G[k], tab, s_q);
+    }
+    const uint32_t s = S.SUCC[k];
+    if (s == SUCC_TERM || s == k) continue;
+    const uint32_t vs = S.V[s];
+    if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) enqueue_pair(P, vs, S.G[k], tab, s_q);
+  }
+  __syncthreads();
+}
+
 // Parallel: the next hop of every agent from the cell its resolved code points at (the pair the
 // movement phase or the next step reads after the agent moves, tswap.rs:263-273); speculative,
 // bounded by half the queue like rules_prefetch.
@@ -367,8 +392,13 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     S.G = P.g;
     S.GT = P.gt;
     S.SUCC = P.succ;
-    S.F1 = P.f1;
-    S.F2 = P.f2;
+    if (P.f_lds) {  // pointer doubling (rules_init) on LDS instead of global memory
+      S.F1 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
+      S.F2 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
+    } else {
+      S.F1 = P.f1;
+      S.F2 = P.f2;
+    }
     S.NHC = P.nhc;
     S.DEC = P.dec;
     S.ONC = P.onc;
@@ -558,9 +588,16 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       if (P.dbg && tid == 0) s_tp = wall_clock64();
       rules_init(P, S);
       if (P.prefetch) rules_prefetch(P, S, &s_q);
+      if (tid == 0) s_cnt = 0;
       PLAN_TICK(15);
       // One firing agent per round (tswap.rs:180-252 in agent order): fire(b) applies b's rule 3
       // swap or rule 4 rotation (tid 0 only) and sets s_miss when next hops must be refreshed.
+      // agents whose goals changed since the last prefetch, in `list` (s_cnt; NO_AGENT = overflow,
+      // the next relabel prefetches for everyone)
+      auto note_changed = [&](uint32_t a) {
+        if (s_cnt < LIST_CAP) list[s_cnt++] = a;
+        else s_cnt = NO_AGENT;
+      };
       auto fire = [&](uint32_t b) {
         const uint32_t s = S.SUCC[b];
         if (S.V[s] == S.G[s]) {  // rule 3: goal swap (tswap.rs:198-202)
@@ -594,6 +631,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             S.NHC[s] = NHC_DIRTY;  // unresolved: refresh + full relabel below
             s_miss = 1;
           }
+          note_changed(b);  // goals of b and s changed (targeted prefetch after the next relabel)
+          note_changed(s);
         } else {  // rule 4: rotate targets along the cycle b -> s -> ... -> last -> b
           uint32_t L = 0;
           // cycle members in S.F2 (free until the rules_init this rotation triggers; LDS when
@@ -613,6 +652,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           S.GT[b] = last_tab;
           S.NHC[b] = NHC_DIRTY;
           s_miss = 1;  // members' next hops changed: refresh + full relabel below
+          for (uint32_t kk = 0; kk < L; ++kk) note_changed(ap[kk]);
         }
         s_ctl.i = b + 1;
         s_ctl.rule_rounds += 1;
@@ -621,7 +661,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // 64 agents from the cursor, the fire is lane 0 of the same wave, so a round needs no
       // workgroup barrier and no cross-wave reduction; the block joins only when a firing
       // changed next hops (refresh + relabel) or the phase ends.
-      const bool wave_scan = n <= 512u;
+      const bool wave_scan = n <= P.wave_rules_max;
       for (;;) {
         if (wave_scan) {
           if (wid == 0) {
@@ -692,7 +732,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             break;
           }
           rules_init(P, S);
-          if (P.prefetch) rules_prefetch(P, S, &s_q);
+          if (P.prefetch) {
+            if (P.wide_prefetch && s_cnt != NO_AGENT) rules_prefetch_list(P, S, &s_q, list, s_cnt);
+            else rules_prefetch(P, S, &s_q);
+          }
+          if (tid == 0) s_cnt = 0;
           PLAN_TICK(15);
         }
       }
@@ -1004,10 +1048,11 @@ __global__ void k_occ_flag(uint32_t* occ, const uint32_t* cnt, uint32_t ncell, u
   }
 }
 
-size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks) {
+size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks, bool flinks) {
   auto r16 = [](size_t b) { return (b + 15u) & ~(size_t)15u; };
   size_t b = r16(1024 * 4);
   if (agents) b += 4 * r16((size_t)n * 4) + 2 * r16((size_t)(n + 1) * 4) + 4 * r16(n);
+  else if (flinks) b += 2 * r16((size_t)(n + 1) * 4);
   if (occ) b += r16((size_t)ncell * 4) + r16((size_t)ncell * 8);
   if (tasks) b += r16((size_t)m * 4) + r16(m);
   return b;
