@@ -598,38 +598,72 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (s_cnt < LIST_CAP) list[s_cnt++] = a;
         else s_cnt = NO_AGENT;
       };
-      auto fire = [&](uint32_t b) {
+      // fire(b) returns what the wave-0 rounds need to update their per-lane firing flags
+      // without re-reading LDS: FO_MISS (codes must be refreshed), FO_RESCAN (a new cycle or a
+      // shared-start goal changed labels: rescan from the cursor), else a rule-3 swap (b, s)
+      // whose only effects on the firing predicate of other agents are s's new successor `ns`
+      // (firing flag `fs`) and the new at-goal status of b (`b_at`) and s (`s_at`).
+      struct FireOut {
+        uint32_t s, ns, flags;
+        bool fs, b_at, s_at;
+      };
+      constexpr uint32_t FO_MISS = 1u, FO_RESCAN = 2u;
+      auto fire = [&](uint32_t b) -> FireOut {
+        FireOut o;
+        o.flags = 0;
+        o.fs = o.b_at = o.s_at = false;
+        o.ns = SUCC_TERM;
         const uint32_t s = S.SUCC[b];
-        if (S.V[s] == S.G[s]) {  // rule 3: goal swap (tswap.rs:198-202)
-          uint32_t code = S.CANDC[b];
-          if (code > NH_STAY && S.GT[b] >= 0) code = P.nh[(uint64_t)S.GT[b] * P.nstride + S.V[s]];
-          const uint32_t gb = S.G[b];
-          const int32_t tb = S.GT[b];
-          S.G[b] = S.G[s];
-          S.GT[b] = S.GT[s];
+        o.s = s;
+        // every load of the swap up front (independent LDS reads, one round trip)
+        const uint32_t vs = S.V[s], gs = S.G[s], vb = S.V[b], gb = S.G[b];
+        const int32_t tb = S.GT[b], ts = S.GT[s];
+        const uint32_t candc = S.CANDC[b];
+        if (vs == gs) {  // rule 3: goal swap (tswap.rs:198-202)
+          uint32_t code = candc;
+          if (code > NH_STAY && tb >= 0) code = P.nh[(uint64_t)tb * P.nstride + vs];  // s's new goal is gb
+          S.G[b] = gs;
+          S.GT[b] = ts;
           S.G[s] = gb;
           S.GT[s] = tb;
           S.CANDC[s] = NHC_DIRTY;
-          if (S.V[b] == S.G[b]) S.SUCC[b] = SUCC_TERM;  // shared start cell: b now at its goal
+          o.b_at = vb == gs;
+          o.s_at = vs == gb;
+          if (o.b_at) {  // shared start cell: b now at its goal
+            S.SUCC[b] = SUCC_TERM;
+            o.flags |= FO_RESCAN;
+          }
           if (code <= NH_STAY) {
             S.NHC[s] = (uint8_t)code;
-            const uint32_t ns = succ_of(P, S, s);
+            // succ_of(s) with the values already in registers
+            uint32_t ns = SUCC_TERM;
+            if (vs != gb) {
+              const uint32_t oc = S.OCC[step_cell(vs, code, P.W)];
+              ns = oc == OCC_NONE ? SUCC_TERM : (oc & OCC_IDX);
+            }
             S.SUCC[s] = ns;
+            o.ns = ns;
             if (ns != SUCC_TERM && ns != s) {
               // new cycle through s?
               uint32_t x = ns;
-              for (uint32_t it = 0; it < n && x != SUCC_TERM && x != s; ++it) x = S.SUCC[x];
+              uint32_t it = 0;
+              for (; it < n && x != SUCC_TERM && x != s; ++it) x = S.SUCC[x];
+              if (P.dbg) s_tick[9] += it;  // diagnostics: rule-3 cycle-walk hops
               if (x == s) {
                 uint32_t y = s;
                 do {
                   S.ONC[y] = 1;
                   y = S.SUCC[y];
                 } while (y != s);
+                o.flags |= FO_RESCAN;
+              } else {
+                o.fs = S.V[ns] == S.G[ns];  // s fires rule 3 next (ONC[s] is 0: s was terminal)
               }
             }
           } else {
             S.NHC[s] = NHC_DIRTY;  // unresolved: refresh + full relabel below
             s_miss = 1;
+            o.flags |= FO_MISS;
           }
           note_changed(b);  // goals of b and s changed (targeted prefetch after the next relabel)
           note_changed(s);
@@ -652,10 +686,13 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           S.GT[b] = last_tab;
           S.NHC[b] = NHC_DIRTY;
           s_miss = 1;  // members' next hops changed: refresh + full relabel below
+          o.flags |= FO_MISS;
           for (uint32_t kk = 0; kk < L; ++kk) note_changed(ap[kk]);
+          if (P.dbg) s_tick[11] += 1;  // diagnostics: rule-4 rotations
         }
         s_ctl.i = b + 1;
         s_ctl.rule_rounds += 1;
+        return o;
       };
       // n <= 512: wave 0 alone runs scan + fire rounds back to back — the scan is a ballot over
       // 64 agents from the cursor, the fire is lane 0 of the same wave, so a round needs no
@@ -665,31 +702,76 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       for (;;) {
         if (wave_scan) {
           if (wid == 0) {
+            // Per-lane state of the chunk [base, base+64): successor sk, ONC bit, firing flag f.
+            // A rule-3 swap (b, s) changes the firing predicate of other agents only through
+            // s's successor and the at-goal status of b and s, which fire() returns in
+            // registers: the flags are updated in place and the next firing agent is the
+            // next set bit of the ballot — no LDS re-scan and no cursor round trip per round.
+            // The firing lane itself applies the swap (its b, s are already in registers).
+            __threadfence_block();
+            uint32_t base = *(volatile uint32_t*)&s_ctl.i;
+            bool loaded = false;
+            uint32_t sk = SUCC_TERM;
+            bool f = false, onck = false;
+            uint64_t m = 0;
             for (;;) {
-              __threadfence_block();
-              const uint32_t cursor = *(volatile uint32_t*)&s_ctl.i;
-              uint32_t b = NO_AGENT;
-              for (uint32_t base = cursor; base < n; base += 64u) {
-                const uint32_t k = base + lane;
-                bool f = false;
-                if (k < n) {
-                  const uint32_t s = S.SUCC[k];
-                  f = s != SUCC_TERM && s != k && (S.V[s] == S.G[s] || S.ONC[k]);
-                }
-                const uint64_t m = __ballot(f);
-                if (m) {
-                  b = base + (uint32_t)__builtin_ctzll(m);
+              if (!loaded) {
+                if (base >= n) {
+                  if (lane == 0) {
+                    s_best = NO_AGENT;
+                    s_ctl.i = n;
+                  }
                   break;
                 }
+                const uint32_t k = base + lane;
+                f = false;
+                onck = false;
+                sk = SUCC_TERM;
+                if (k < n) {
+                  sk = S.SUCC[k];
+                  onck = S.ONC[k] != 0;
+                  f = sk != SUCC_TERM && sk != k && (S.V[sk] == S.G[sk] || onck);
+                }
+                m = __ballot(f);
+                loaded = true;
               }
-              if (lane == 0) {
+              if (!m) {
+                base += 64u;
+                loaded = false;
+                continue;
+              }
+              const uint32_t l = (uint32_t)__builtin_ctzll(m);
+              const uint32_t b = base + l;
+              uint32_t r_fl = 0, r_s = 0, r_ns = 0, r_bits = 0;
+              if (lane == l) {
                 s_best = b;
                 s_miss = 0;
-                if (b != NO_AGENT) fire(b);
-                else s_ctl.i = n;
+                const FireOut r = fire(b);
+                r_fl = r.flags;
+                r_s = r.s;
+                r_ns = r.ns;
+                r_bits = (r.fs ? 1u : 0u) | (r.b_at ? 2u : 0u) | (r.s_at ? 4u : 0u);
               }
               __threadfence_block();
-              if (b == NO_AGENT || *(volatile uint32_t*)&s_miss) break;
+              const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)r_fl, (int)l);
+              if (fl & FO_MISS) break;
+              if (fl & FO_RESCAN) {
+                base = b + 1u;
+                loaded = false;
+                continue;
+              }
+              const uint32_t fs_ = (uint32_t)__builtin_amdgcn_readlane((int)r_s, (int)l);
+              const uint32_t fns = (uint32_t)__builtin_amdgcn_readlane((int)r_ns, (int)l);
+              const uint32_t fbits = (uint32_t)__builtin_amdgcn_readlane((int)r_bits, (int)l);
+              const uint32_t k = base + lane;
+              if (k == fs_) {
+                sk = fns;
+                f = (fbits & 1u) != 0;
+              } else if (sk != SUCC_TERM && sk != k) {
+                if (sk == fs_) f = (fbits & 4u) != 0 || onck;
+                else if (sk == b) f = (fbits & 2u) != 0 || onck;
+              }
+              m = __ballot(f) & ~((2ull << l) - 1ull);  // l == 63: shift wraps to 0, mask 0
             }
           }
         } else {
