@@ -37,6 +37,7 @@ struct DevStatus {
   uint32_t novf;  // LDS A*: queries handed to the global-heap kernel
   uint32_t novf2;  // second tier (LDS heap, global g_scores): queries handed on to k_astar
   uint32_t work;  // k_bfs_wave goal dequeue counter
+  uint32_t qnext;  // k_astar_lds dynamic query dequeue counter
 };
 
 enum { CAT_BFS = 0, CAT_ASTAR = 1, CAT_WALK = 2, CAT_ASSIGN = 3, NCAT = 4 };
@@ -370,8 +371,9 @@ int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint
       HIPCHK(dgrow(c->d_ovf, c->ovf_cap, nq));
     }
     HIPCHK(hipMemsetAsync(&c->d_stat->novf, 0, 4, c->s));
+    HIPCHK(hipMemsetAsync(&c->d_stat->qnext, 0, 4, c->s));
     HIPCHK(launch_astar_lds(c->G, Q, nq, nh, c->tstride, res, lens, c->d_gs16, c->d_ep16, c->nslots16, c->d_ovf,
-                            &c->d_stat->novf, c->s));
+                            &c->d_stat->novf, &c->d_stat->qnext, c->s));
     HIPCHK(hipMemcpyAsync(&c->h_stat->novf, &c->d_stat->novf, 4, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     const uint32_t novf = c->h_stat->novf;
@@ -420,7 +422,11 @@ int resolve_all_unknown(tsw_ctx* c, const std::vector<uint32_t>& goals, const st
   TRY(ensure_tmp(c, goals.size()));
   HIPCHK(hipMemcpyAsync(c->d_tmp_a, goals.data(), goals.size() * 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
-  TRY(ensure_queue(c, std::max<size_t>(c->qcap, 1u << 16)));
+  // one queue for every pair of the batch (eager_policy bounds it to 8M): a single K3 launch
+  // gives each lane several queries, so the launch is not the longest query times the number
+  // of 64k-query batches
+  const size_t bound = std::min<size_t>((size_t)goals.size() * c->G.ncell, (size_t)1 << 23);
+  TRY(ensure_queue(c, std::max<size_t>({c->qcap, (size_t)1 << 16, bound})));
   for (int iter = 0; iter < 1000000; ++iter) {
     HIPCHK(hipMemsetAsync(&c->d_stat->qcount, 0, 4, c->s));
     HIPCHK(launch_enqueue_unknown(c->G, c->d_tmp_a, c->d_tmp_b, (uint32_t)goals.size(), c->d_nh, c->tstride,

@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(LDS_BLK) k_astar_lds(DevGrid G, const AstarQue
                                                         uint8_t* __restrict__ res, int32_t* __restrict__ lens,
                                                         uint16_t* __restrict__ gs_all, uint32_t* __restrict__ epochs,
                                                         uint32_t nslots, AstarQuery* __restrict__ ovf,
-                                                        uint32_t* __restrict__ novf) {
+                                                        uint32_t* __restrict__ novf, uint32_t* __restrict__ qnext) {
   __shared__ uint32_t Hs[LDS_HCAP * LDS_BLK];
   const uint32_t t = threadIdx.x;
   const uint32_t slot = blockIdx.x * LDS_BLK + t;
@@ -402,7 +402,9 @@ __global__ void __launch_bounds__(LDS_BLK) k_astar_lds(DevGrid G, const AstarQue
   const float invW = 1.0f / (float)W;
   uint16_t* GS = gs_all + (uint64_t)slot * ncell;
   uint32_t ep = epochs[slot];
-  for (uint32_t qi = slot; qi < nq; qi += nslots) {
+  // first query static (qi = slot), then dynamic dequeue: query times vary by orders of
+  // magnitude, so lanes that finish early take the rest instead of a fixed stride
+  for (uint32_t qi = slot; qi < nq; qi = nslots + atomicAdd(qnext, 1u)) {
     if (ep % 15u == 0u && ep > 0u)
       for (uint32_t c = 0; c < ncell; ++c) GS[c] = 0;
     const uint32_t tagw = (ep % 15u + 1u) << 12;
@@ -1059,12 +1061,12 @@ hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* n
 
 hipError_t launch_astar_lds(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
                             uint8_t* res, int32_t* lens, uint16_t* gs16, uint32_t* epochs, uint32_t nslots,
-                            AstarQuery* ovf, uint32_t* novf, hipStream_t s) {
+                            AstarQuery* ovf, uint32_t* novf, uint32_t* qnext, hipStream_t s) {
   if (nq == 0) return hipSuccess;
   const uint32_t th = std::min(nq, nslots);
   const uint32_t grid = (th + LDS_BLK - 1) / LDS_BLK;
   hipLaunchKernelGGL(k_astar_lds, dim3(grid), dim3(LDS_BLK), 0, s, G, Q, nq, nh_base, nstride, res, lens, gs16,
-                     epochs, th, ovf, novf);
+                     epochs, th, ovf, novf, qnext);
   return hipGetLastError();
 }
 

@@ -75,7 +75,7 @@ hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* n
 bool astar_lds_ok(const DevGrid& G);
 hipError_t launch_astar_lds(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
                             uint8_t* res, int32_t* lens, uint16_t* gs16, uint32_t* epochs, uint32_t nslots,
-                            AstarQuery* ovf, uint32_t* novf, hipStream_t s);
+                            AstarQuery* ovf, uint32_t* novf, uint32_t* qnext, hipStream_t s);
 
 // One query per wave, LDS heap (grids of > 1024 cells); gs_all/epochs: nslots u32 g_score
 // arrays of ncell words (used only when the grid's g_scores do not fit LDS).
