@@ -37,7 +37,8 @@ struct DevStatus {
   uint32_t novf;  // LDS A*: queries handed to the global-heap kernel
   uint32_t novf2;  // second tier (LDS heap, global g_scores): queries handed on to k_astar
   uint32_t work;  // k_bfs_wave goal dequeue counter
-  uint32_t qnext;  // k_astar_lds dynamic query dequeue counter
+  uint32_t qnext;  // k_astar_lds / k_astar_wave dynamic query dequeue counter
+  uint32_t qnext2;  // k_astar_wave second tier
 };
 
 enum { CAT_BFS = 0, CAT_ASTAR = 1, CAT_WALK = 2, CAT_ASSIGN = 3, NCAT = 4 };
@@ -388,10 +389,11 @@ int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint
       HIPCHK(dgrow(c->d_ovf, c->ovf_cap, nq));
       HIPCHK(dgrow(c->d_ovf2, cap2, c->ovf_cap));
     }
-    HIPCHK(hipMemsetAsync(&c->d_stat->novf, 0, 8, c->s));  // novf, novf2
+    HIPCHK(hipMemsetAsync(&c->d_stat->novf, 0, 8, c->s));   // novf, novf2
+    HIPCHK(hipMemsetAsync(&c->d_stat->qnext, 0, 8, c->s));  // qnext, qnext2
     const uint32_t slots = std::min(astar_wave_slots(c->G, c->num_cu), c->nslots);
     HIPCHK(launch_astar_wave(c->G, Q, nq, nh, c->tstride, res, lens, c->d_gs, c->d_epochs, slots, c->d_ovf,
-                             &c->d_stat->novf, c->wave_hcap, false, c->s));
+                             &c->d_stat->novf, c->wave_hcap, false, c->s, &c->d_stat->qnext));
     HIPCHK(hipMemcpyAsync(&c->h_stat->novf, &c->d_stat->novf, 4, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     uint32_t novf = c->h_stat->novf;
@@ -401,7 +403,7 @@ int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint
       // the global u32 slots while the heap stays in LDS; only heap overflows reach k_astar
       const uint32_t slots2 = std::min(astar_wave_slots(c->G, c->num_cu, true), c->nslots);
       HIPCHK(launch_astar_wave(c->G, c->d_ovf, novf, nh, c->tstride, res, lens, c->d_gs, c->d_epochs, slots2,
-                               c->d_ovf2, &c->d_stat->novf2, c->wave_hcap, true, c->s));
+                               c->d_ovf2, &c->d_stat->novf2, c->wave_hcap, true, c->s, &c->d_stat->qnext2));
       HIPCHK(hipMemcpyAsync(&c->h_stat->novf2, &c->d_stat->novf2, 4, hipMemcpyDeviceToHost, c->s));
       HIPCHK(hipStreamSynchronize(c->s));
       novf = c->h_stat->novf2;

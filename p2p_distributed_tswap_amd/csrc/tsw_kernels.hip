@@ -911,7 +911,8 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
                                                    uint32_t hcap, uint32_t gs_lds, uint32_t* __restrict__ gs_all,
                                                    uint32_t* __restrict__ epochs, AstarQuery* __restrict__ ovf,
                                                    uint32_t* __restrict__ novf, uint32_t serial,
-                                                   unsigned long long* __restrict__ prof) {
+                                                   unsigned long long* __restrict__ prof,
+                                                   uint32_t* __restrict__ qnext) {
   extern __shared__ __align__(16) uint64_t wsm[];
   uint64_t* Hp = wsm;
   const uint32_t lane = threadIdx.x, ncell = G.ncell;
@@ -928,7 +929,15 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
   if (gs_lds == 1u)
     for (uint32_t c = lane; c < ncell; c += 64u) GS[c] = 0u;
   __syncthreads();
-  for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+  // first query static (qi = block), then dynamic dequeue (lane 0's atomic, read by the whole
+  // wave): a batch's query times vary by orders of magnitude, a fixed stride idles waves
+  auto next_q = [&](uint32_t qi) -> uint32_t {
+    if (!qnext) return qi + gridDim.x;
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(qnext, 1u);
+    return gridDim.x + (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+  };
+  for (uint32_t qi = blockIdx.x; qi < nq; qi = next_q(qi)) {
     if (gs_lds == 2u) {
       uint4* g4 = reinterpret_cast<uint4*>(GB);
       for (uint32_t c = lane; c < (ncell + 15u) / 16u; c += 64u) g4[c] = make_uint4(0u, 0u, 0u, 0u);
@@ -1106,7 +1115,8 @@ uint32_t astar_wave_slots(const DevGrid& G, int num_cu, bool global_gs) {
 
 hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
                              uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
-                             AstarQuery* ovf, uint32_t* novf, uint32_t hcap, bool global_gs, hipStream_t s) {
+                             AstarQuery* ovf, uint32_t* novf, uint32_t hcap, bool global_gs, hipStream_t s,
+                             uint32_t* qnext) {
   if (nq == 0) return hipSuccess;
   const uint32_t gs_lds = global_gs ? 0u : wave_gs_mode(G);
   hcap = hcap ? std::max<uint32_t>(4u, std::min(hcap, WAVE_HCAP)) : WAVE_HCAP;
@@ -1124,7 +1134,7 @@ hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq,
     hipMemsetAsync(prof, 0, (size_t)nq * 64u, s);
   }
   hipLaunchKernelGGL(k_astar_wave, dim3(grid), dim3(64), lds, s, G, Q, nq, nh_base, nstride, res, lens, hcap,
-                     gs_lds, gs_all, epochs, ovf, novf, serial, prof);
+                     gs_lds, gs_all, epochs, ovf, novf, serial, prof, qnext);
   e = hipGetLastError();
   if (prof) {
     std::vector<unsigned long long> h((size_t)nq * 8u);

@@ -86,7 +86,7 @@ bool astar_wave_lds_gs(const DevGrid& G);  // k_astar_wave keeps this grid's g_s
 hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
                              uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
                              AstarQuery* ovf, uint32_t* novf, uint32_t hcap /*0: default*/, bool global_gs,
-                             hipStream_t s);
+                             hipStream_t s, uint32_t* qnext = nullptr);
 
 // Batched decentralized decision (tsw_decide.hip, agent.rs:329-462).
 constexpr uint32_t DEC_ACT_MOVE = 0, DEC_ACT_GOAL_SWAP = 1, DEC_ACT_ROTATION = 2, DEC_ACT_WAIT = 3;
