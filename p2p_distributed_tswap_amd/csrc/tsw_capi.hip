@@ -391,9 +391,17 @@ int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint
     }
     HIPCHK(hipMemsetAsync(&c->d_stat->novf, 0, 8, c->s));   // novf, novf2
     HIPCHK(hipMemsetAsync(&c->d_stat->qnext, 0, 8, c->s));  // qnext, qnext2
-    const uint32_t slots = std::min(astar_wave_slots(c->G, c->num_cu), c->nslots);
+    // g_scores in LDS cap residency (the byte words of a 510x220 grid are 112 KB: one wave per
+    // CU). When the batch has more queries than LDS-resident waves, throughput wins: keep only
+    // the heap in LDS and the g_scores in the global slots (3-4 waves per CU; wh10k prefix
+    // 3.32 -> 2.68 s); a smaller batch is bound by its slowest query, where LDS g_scores are
+    // faster per pop. TSW_ASTAR_GLOBAL_GS=0/1 forces either (A/B).
+    const char* ge = getenv("TSW_ASTAR_GLOBAL_GS");
+    const bool ggs = ge ? atoi(ge) != 0
+                        : astar_wave_lds_gs(c->G) && nq > std::min(astar_wave_slots(c->G, c->num_cu), c->nslots);
+    const uint32_t slots = std::min(astar_wave_slots(c->G, c->num_cu, ggs), c->nslots);
     HIPCHK(launch_astar_wave(c->G, Q, nq, nh, c->tstride, res, lens, c->d_gs, c->d_epochs, slots, c->d_ovf,
-                             &c->d_stat->novf, c->wave_hcap, false, c->s, &c->d_stat->qnext));
+                             &c->d_stat->novf, c->wave_hcap, ggs, c->s, &c->d_stat->qnext));
     HIPCHK(hipMemcpyAsync(&c->h_stat->novf, &c->d_stat->novf, 4, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     uint32_t novf = c->h_stat->novf;
