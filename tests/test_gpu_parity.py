@@ -288,3 +288,42 @@ def test_astar_wave_cores_and_tiers(monkeypatch, mode):
     for q in range(s.size):
         rn, rl, _ = og.get_path_next(int(s[q]), int(g[q]))
         assert (nxt[q], ln[q]) == (rn, rl), f"query {s[q]}->{g[q]} ({mode})"
+
+
+@pytest.mark.parametrize("gs", ["auto", "lds", "global"])
+def test_astar_wave_batch_gscore_placement(monkeypatch, gs):
+    """A k_astar_wave batch with several queries per wave (dynamic dequeue) and the g-scores in
+    LDS (small batches), in the global slots (batches larger than the LDS-resident waves, the
+    default then) or forced either way: bit-exact on the 170x84 warehouse."""
+    if gs != "auto":
+        monkeypatch.setenv("TSW_ASTAR_GLOBAL_GS", "1" if gs == "global" else "0")
+    rows = _grid("warehouse")
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@"))
+    rng = np.random.default_rng(13)
+    nq = 3000
+    s = rng.choice(free, nq).astype(np.uint32)
+    g = rng.choice(free, nq).astype(np.uint32)
+    with Planner(rows) as p:
+        nxt, ln = p.get_path_next(s, g)
+    bad = [q for q in range(nq) if (nxt[q], ln[q]) != og.get_path_next(int(s[q]), int(g[q]))[:2]]
+    assert not bad, f"{len(bad)} mismatches ({gs}), first {bad[:5]}"
+
+
+def test_astar_lds_more_queries_than_slots():
+    """k_astar_lds (<= 1024 cells) with more queries than its 65,536 lane slots: the dynamic
+    dequeue hands the surplus to lanes that finished early; every answer bit-exact."""
+    rows = _grid("rand32")
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@"))
+    rng = np.random.default_rng(17)
+    nq = 70000
+    s = rng.choice(free, nq).astype(np.uint32)
+    g = rng.choice(free, nq).astype(np.uint32)
+    with Planner(rows) as p:
+        nxt, ln = p.get_path_next(s, g)
+    idx = np.concatenate([np.arange(0, nq, 7), np.arange(65536, nq)])  # surplus checked in full
+    bad = [int(q) for q in idx if (nxt[q], ln[q]) != og.get_path_next(int(s[q]), int(g[q]))[:2]]
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
