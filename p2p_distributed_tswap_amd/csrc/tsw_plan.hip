@@ -276,6 +276,16 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
   const uint32_t tid = threadIdx.x, bd = blockDim.x, hops = P.wide_prefetch ? P.wide_prefetch : 1u;
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (*(volatile uint32_t*)s_q >= P.qcap / 2u) break;
+    // heading to a pickup: the pair the state machine needs on arrival (goal := delivery,
+    // tswap.rs:113-118) is known since the assignment — (pickup cell, delivery goal)
+    if (P.mode != MODE_STEP && P.m > 0 && P.st[k] == ST_TO_PICKUP) {
+      const int32_t tk = P.task[k];
+      if (tk >= 0 && (uint32_t)tk < P.m) {
+        const uint32_t pc = P.pick[tk], dc = P.dlv[tk];
+        const int32_t dt = P.goal_tab[dc];
+        if (dt >= 0 && pc != dc && P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) enqueue_pair(P, pc, dc, dt, s_q);
+      }
+    }
     const int32_t tab = S.GT[k];
     const uint8_t c = S.NHC[k];
     if (tab < 0 || c >= NH_STAY || S.V[k] == S.G[k]) continue;
