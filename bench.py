@@ -3,21 +3,28 @@
 Contract (driver): python bench.py --gpus N --steps K --warmup W ; for N > 1 it is
 launched under torch.distributed.run, one rank per GPU. Rank 0 prints ONE JSON line.
 
-Workload (BASELINE.json configs[1]): random-32-32-20 grid (Bernoulli 0.20, seed 0x3232),
-200 agents, 600-task MAPD stream, reference step cap (timestep > 2000). One bench "step"
-= one complete tsw_plan_mapd over that instance from an empty table store: K1 BFS tables
-for every goal cell, next-hop resolution (K3 A*), then every timestep's K4 assign ->
-K2 step -> record on the device. value = agent-steps (n x T summed over ranks) / max-over-
-ranks wall time of the K timed steps. N > 1: the planning step does not shard (sequential
-agent order), so each rank plans its own replica (seed + rank) — weak scaling.
+Workload: BASELINE.json configs[2], the largest single-GPU planning config — warehouse-like
+170x84 grid (shelf blocks, 1-wide aisles, seed 0x170084), 1,000 agents, 3,000-task MAPD stream,
+reference step cap (timestep > 2000). One bench "step" = one complete tsw_plan_mapd over that
+instance from an empty table store: K1 BFS tables for every goal cell, next-hop resolution (K3
+exact A*), then every timestep's K4 assign -> K2 step -> record on the device. The instance
+(a few KB of host arrays) is handed over through the C ABI like the reference's
+`tswap_mapd(grid, starts, tasks)`. value = agent-steps (n x T summed over ranks) / max-over-ranks
+wall time of the K timed steps. N > 1: the planning step does not shard (sequential agent order,
+SURVEY.md §8e), so each rank plans its own replica (seed + rank) — weak scaling.
 
 Extra objects on the line:
-  roofline      for the kernel with the most device time inside the timed steps, from
-                HIP events on the library's stream (tsw_get_stats).
+  roofline      the kernel class with the most device time inside the timed steps (HIP events
+                on the library's stream, tsw_get_stats), algorithmic bytes per launch, and the
+                PMC traffic per launch from profiles/<PROFILE_TAG>/pmc.json — only when that file
+                was measured on THIS workload (same algorithmic bytes per launch), else null.
+  latency       K3 and k_plan against their latency floors (they are serial-dependency bound,
+                not bandwidth bound; see DESIGN.md "Latency rooflines").
   bfs           K1 alone on a den520d-like 256x257 cave, 10,000 distinct goals (configs[3]),
                 cells/s and fraction of the 8 TB/s HBM peak (algorithmic bytes).
-  cpu_baseline  the oracle (faithful single-thread C restatement of tswap.rs) on the same
-                instance, rank 0 only.
+  cpu_baseline  the oracle (faithful single-thread C restatement of tswap.rs) planning a bounded
+                prefix of the same instance on one pinned host core, rank 0 only; its prefix is
+                also compared bit-exactly with the GPU plan.
 """
 from __future__ import annotations
 
@@ -32,7 +39,9 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md:36
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md ("HBM: 8 TB/s peak")
+PROFILE_TAG = "r2"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
+BFS_WORKLOAD = "bfs:den520d_10k"
 
 
 def parse():
@@ -42,9 +51,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-bfs", action="store_true", help="skip the K1 BFS measurement")
+    ap.add_argument("--no-plan", action="store_true", help="skip the planning leg (profiling K1 alone)")
     ap.add_argument("--bfs-goals", type=int, default=10000)
     ap.add_argument("--bfs-reps", type=int, default=3)
-    ap.add_argument("--config", default="c2_random_32_32_20")
+    ap.add_argument("--cpu-steps", type=int, default=300,
+                    help="timesteps of the CPU baseline's prefix (bounded sample of the same plan)")
+    ap.add_argument("--config", default="c3_warehouse_170x84")
     ap.add_argument("--nexthop", choices=("auto", "eager", "lazy"), default="auto",
                     help="next-hop resolution policy (TSW_F_EAGER_NEXTHOP / TSW_F_LAZY_NEXTHOP)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -52,23 +64,22 @@ def parse():
     return ap.parse_args()
 
 
-def profiled_traffic(kernel_prefix: str):
-    """Per-launch HBM bytes of a kernel from the newest committed PMC summary
-    (profiles/<round>/summary.json, made by scripts/profile_round.sh + summarize_profile.py:
-    separate FETCH_SIZE / WRITE_SIZE passes, gfx950 FETCH_SIZE x2 correction)."""
-    import glob
-
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "summary.json")), key=os.path.getmtime)
-    for p in reversed(paths):
-        try:
-            with open(p) as f:
-                ks = json.load(f)["kernels"]
-        except (OSError, ValueError, KeyError):
-            continue
-        for name, d in ks.items():
-            if name.startswith(kernel_prefix) and "hbm_bytes_per_launch" in d:
-                return float(d["hbm_bytes_per_launch"]), os.path.relpath(p, ROOT)
-    return None, None
+def profiled_traffic(workload: str, kclass: str, algo_bytes_per_launch: float):
+    """HBM bytes per launch of kernel class `kclass` measured by PMC on `workload`
+    (profiles/<PROFILE_TAG>/pmc.json, written by scripts/summarize_profile.py from separate
+    FETCH_SIZE / WRITE_SIZE passes with the gfx950 FETCH_SIZE x2 correction). Returned only if the
+    profiled run had the same algorithmic bytes per launch (within 2 %): a profile of another
+    workload never feeds this line."""
+    p = os.path.join(ROOT, "profiles", PROFILE_TAG, "pmc.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)["workloads"][workload][kclass]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    a = float(d.get("algorithmic_bytes_per_launch", 0.0))
+    if a <= 0 or abs(a - algo_bytes_per_launch) > 0.02 * algo_bytes_per_launch or "hbm_bytes_per_launch" not in d:
+        return None, None
+    return float(d["hbm_bytes_per_launch"]), os.path.relpath(p, ROOT)
 
 
 def bfs_bytes_per_goal(w: int, h: int, with_nh: bool) -> int:
@@ -76,6 +87,51 @@ def bfs_bytes_per_goal(w: int, h: int, with_nh: bool) -> int:
     + the obstacle bitmap read."""
     cells = w * h
     return cells * 2 + (cells if with_nh else 0) + (cells + 7) // 8
+
+
+def host_cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(rows, starts, tasks, n_agents, steps, gpu_rec):
+    """The C oracle (single thread, -O2) planning the first `steps` timesteps of the same instance,
+    pinned to one host core (sched_setaffinity = taskset -c <core>), compared with the GPU plan."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleGraph  # CPU baseline (and prefix check) only
+
+    og = OracleGraph(np.frombuffer("".join(rows).encode("latin-1"), dtype=np.uint8).reshape(len(rows), -1))
+    old = os.sched_getaffinity(0)
+    core = min(old)
+    os.sched_setaffinity(0, {core})
+    try:
+        tc = time.perf_counter()
+        rec, _ = og.mapd(starts, tasks, steps)
+        tcd = time.perf_counter() - tc
+    finally:
+        os.sched_setaffinity(0, old)
+    T = rec.shape[1]
+    return {
+        "value": round(n_agents * T / tcd, 1),
+        "unit": "agent-steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"first {T} timesteps of the same plan ({n_agents} agents x {T} = {n_agents * T} agent-steps, "
+                   f"{tcd:.2f} s), oracle/tswap_oracle.c -O2, one thread pinned to core {core} "
+                   f"(sched_setaffinity, = taskset -c {core})"),
+        "host_cpu": host_cpu_model(),
+        "host_cores_total": os.cpu_count(),
+        "host_cores_allowed": len(old),
+        "prefix_bit_exact_vs_gpu": bool(gpu_rec is not None and np.array_equal(rec, gpu_rec[:, :T])),
+        "note": ("a C port with dense stamped arrays (no HashMap) and the Rust std BinaryHeap restated: "
+                 "likely faster than the Rust original, so the GPU/CPU ratio is conservative"),
+    }
 
 
 def main():
@@ -95,7 +151,7 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    from p2p_distributed_tswap_amd import Planner, maps
+    from p2p_distributed_tswap_amd import TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP, Planner, maps
 
     def barrier():
         if dist is not None:
@@ -120,70 +176,82 @@ def main():
     rows = fac()
     h, w = len(rows), len(rows[0])
     starts, tasks = maps.make_instance(rows, n_agents, n_tasks, seed + rank)
-    from p2p_distributed_tswap_amd import TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP
+    workload = f"plan:{args.config}"
 
-    pflags = {"auto": 0, "eager": TSW_F_EAGER_NEXTHOP, "lazy": TSW_F_LAZY_NEXTHOP}[args.nexthop]
-    planner = Planner(rows, device=dev, flags=pflags)
+    value = dt_max = None
+    Ts, st, roofline, latency, last_rec = [], {}, None, None, None
+    if not args.no_plan:
+        pflags = {"auto": 0, "eager": TSW_F_EAGER_NEXTHOP, "lazy": TSW_F_LAZY_NEXTHOP}[args.nexthop]
+        planner = Planner(rows, device=dev, flags=pflags)
 
-    def one_plan():
-        planner.clear_tables()
-        rec, _ = planner.plan_mapd_arrays(starts, tasks, 2000)
-        return rec.shape[1]
+        def one_plan():
+            planner.clear_tables()
+            rec, _ = planner.plan_mapd_arrays(starts, tasks, 2000)
+            return rec
 
-    for _ in range(args.warmup):
-        one_plan()
-    planner.reset_stats()
-    barrier()
-    t0 = time.perf_counter()
-    agent_steps = 0
-    Ts = []
-    for _ in range(args.steps):
-        T = one_plan()
-        Ts.append(T)
-        agent_steps += n_agents * T
-    barrier()
-    dt = time.perf_counter() - t0
-    st = planner.stats()
-    dt_max = allmax(dt)
-    total_units = allsum(float(agent_steps))
-    value = total_units / dt_max
+        for _ in range(args.warmup):
+            one_plan()
+        planner.reset_stats()
+        barrier()
+        t0 = time.perf_counter()
+        agent_steps = 0
+        for _ in range(args.steps):
+            last_rec = one_plan()
+            Ts.append(int(last_rec.shape[1]))
+            agent_steps += n_agents * last_rec.shape[1]
+        barrier()
+        dt = time.perf_counter() - t0
+        st = planner.stats()
+        dt_max = allmax(dt)
+        value = allsum(float(agent_steps)) / dt_max
+        planner.close()
 
-    # dominant kernel inside the timed region (device time from HIP events)
-    cats = {
-        "k_astar (K3 exact A* next hop)": (st["astar_ms"], st["astar_launches"]),
-        "k_plan (K2 tswap_step + K4 assignment, persistent)": (st["walker_ms"], st["walker_launches"]),
-        "k_bfs (K1 BFS tables + next-hop codes)": (st["bfs_ms"], st["bfs_launches"]),
-    }
-    dom = max(cats, key=lambda k: cats[k][0])
-    dom_ms, dom_launches = cats[dom]
-    avg_launch_ms = dom_ms / max(dom_launches, 1)
-    steps_total = st["steps"]
-    if dom.startswith("k_bfs"):
-        per_launch_bytes = bfs_bytes_per_goal(w, h, True) * st["bfs_goals"] / max(st["bfs_launches"], 1)
-    else:
-        # ~46 B per agent-step for the step/assign kernels; per launch =
-        # agent-steps covered by one launch of that kernel
-        per_launch_bytes = 46.0 * n_agents * steps_total / max(dom_launches, 1)
-    achieved = per_launch_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    traffic, traffic_src = profiled_traffic(dom.split()[0])
-    roofline = {
-        "kernel": dom,
-        "bound": "hbm",
-        "achieved": round(achieved, 3),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 6),
-        "traffic": traffic,
-        "traffic_source": traffic_src,
-        "avg_launch_us": round(avg_launch_ms * 1e3, 3),
-        "launches": int(dom_launches),
-        "note": ("k_plan is one persistent workgroup executing tswap_step's sequential agent-order "
-                 "semantics (tswap.rs:180-285) as exact parallel rounds; it is latency/barrier-bound, "
-                 "so its HBM fraction is tiny by construction. K1 (bfs.roofline) is the HBM-bound kernel."
-                 if dom.startswith("k_plan") else None),
-        "algorithmic_bytes_per_launch": round(per_launch_bytes, 1),
-        "device_ms_by_kernel": {k.split()[0]: round(v[0], 3) for k, v in cats.items()},
-    }
+        # kernel classes inside the timed region (device time from HIP events on the library stream)
+        steps_total = st["steps"]
+        cats = {
+            "K3": ("k_astar_wave / k_astar_lds / k_astar (exact A* next hop, get_path tswap.rs:288-390)",
+                   st["astar_ms"], st["astar_launches"],
+                   # per pass: every query read (16 B) + its next-hop code written (1 B)
+                   17.0 * st["astar_queries"] / max(st["astar_launches"], 1)),
+            "k_plan": ("k_plan (K2 tswap_step + K4 assignment, persistent, tswap.rs:104-286)",
+                       st["walker_ms"], st["walker_launches"],
+                       # ~46 B per agent-step
+                       46.0 * n_agents * steps_total / max(st["walker_launches"], 1)),
+            "K1": ("k_bfs_blk + k_classify (BFS tables + next-hop codes)", st["bfs_ms"], st["bfs_launches"],
+                   bfs_bytes_per_goal(w, h, True) * st["bfs_goals"] / max(st["bfs_launches"], 1)),
+        }
+        dom = max(cats, key=lambda k: cats[k][1])
+        name, dom_ms, dom_launches, per_launch_bytes = cats[dom]
+        avg_launch_ms = dom_ms / max(dom_launches, 1)
+        achieved = per_launch_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+        traffic, traffic_src = profiled_traffic(workload, dom, per_launch_bytes)
+        roofline = {
+            "kernel": name,
+            "bound": "hbm",
+            "achieved": round(achieved, 4),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 8),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "avg_launch_us": round(avg_launch_ms * 1e3, 3),
+            "launches": int(dom_launches),
+            "algorithmic_bytes_per_launch": round(per_launch_bytes, 1),
+            # every kernel class of the timed plans (scripts/summarize_profile.py pairs these with PMC)
+            "classes": {k: {"device_ms": round(v[1], 3), "launches": int(v[2]),
+                            "algorithmic_bytes_per_launch": round(v[3], 1)} for k, v in cats.items()},
+            "note": ("K3 and k_plan move a few bytes per serial heap / commit step: their HBM fraction is tiny by "
+                     "construction and their binding limit is latency (see `latency`). K1 (bfs.roofline) is the "
+                     "HBM-bound kernel." if dom != "K1" else None),
+        }
+        latency = {
+            "k3_pops": st.get("astar_pops", 0),
+            "k3_critical_pops": st.get("astar_crit_pops", 0),
+            "k3_ms": round(st["astar_ms"], 3),
+            "k_plan_ms": round(st["walker_ms"], 3),
+            "plan_exits": st["plan_exits"],
+            "rule_rounds": st["rule_rounds"],
+        }
 
     # K1 BFS alone, den520d-like, 10k distinct goals (configs[3]); rank-local shard of the goals
     bfs = None
@@ -227,7 +295,8 @@ def main():
             del full
         cells_per_s = allsum(float(mine.size * ncell)) * args.bfs_reps / tbw
         k_gbs = mine.size * bytes_goal / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
-        btraffic, btraffic_src = profiled_traffic("k_bfs_blk")
+        algo_launch = float(mine.size * bytes_goal)
+        btraffic, btraffic_src = profiled_traffic(BFS_WORKLOAD, "K1", algo_launch) if world == 1 else (None, None)
         bfs = {
             "workload": "den520d-like 256x257 cave (seed 0x520D), distinct goals",
             "goals_total": int(goals.size),
@@ -246,9 +315,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(k_gbs / HBM_PEAK_GBS, 4),
-                "traffic": btraffic if world == 1 else None,
-                "traffic_source": btraffic_src if world == 1 else None,
-                "algorithmic_bytes_per_launch": int(mine.size * bytes_goal),
+                "traffic": btraffic,
+                "traffic_source": btraffic_src,
+                "algorithmic_bytes_per_launch": int(algo_launch),
             },
             # N > 1: wall time of (this rank's K1 shard + RCCL all-gather of all tables), max over ranks
             "sharded_build_allgather_ms": round(gather_ms, 3) if gather_ms is not None else None,
@@ -257,49 +326,36 @@ def main():
         cp.close()
 
     cpu = None
-    if rank == 0 and not args.no_cpu:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        from oracle import OracleGraph  # CPU baseline only
-
-        og = OracleGraph(maps.rows_to_array(rows))
-        tc = time.perf_counter()
-        rec, _ = og.mapd(starts, tasks, 2000)
-        tcd = time.perf_counter() - tc
-        cpu = {
-            "value": round(n_agents * rec.shape[1] / tcd, 1),
-            "unit": "agent-steps/s",
-            "cores": 1,
-            "kind": "port",
-            "sample": f"1 full plan of the same instance ({n_agents} agents x {rec.shape[1]} timesteps, "
-                      f"{tcd:.2f} s, single thread, oracle/tswap_oracle.c -O2)",
-        }
+    if rank == 0 and not args.no_cpu and not args.no_plan:
+        cpu = cpu_baseline(rows, starts, tasks, n_agents, args.cpu_steps, last_rec)
 
     if rank == 0:
         line = {
             "metric": "TSWAP agent-steps/sec + BFS cells/sec (% HBM peak) at 1/2/4/8 GPUs",
-            "value": round(value, 1),
+            "value": round(value, 1) if value is not None else None,
             "unit": "agent-steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt_max / args.steps * 1e3, 3),
+            "ms_per_step": round(dt_max / args.steps * 1e3, 3) if dt_max is not None else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (seeded random-32-32-20 map and MAPD task stream; replicas seed+rank)",
+            "data": "synthetic (seeded warehouse-like map and MAPD task stream; replicas seed+rank)",
             "config": {
-                "workload": "random-32-32-20, 200 agents, 600-task MAPD stream, cap 2000 (BASELINE configs[1])",
+                "workload": (f"{args.config}: {w}x{h} grid, {n_agents} agents, {n_tasks}-task MAPD stream, "
+                             "cap 2000, full plan from an empty table store per step (BASELINE configs[2])"),
                 "agents": n_agents, "tasks": n_tasks, "grid": f"{w}x{h}",
                 "timesteps_per_plan": Ts, "parallelism": f"replicas x{world} (step not shardable)",
             },
             "roofline": roofline,
+            "latency": latency,
             "bfs": bfs,
             "cpu_baseline": cpu,
             "kernel_stats": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
         }
         print(json.dumps(line), flush=True)
-    planner.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -12,9 +12,31 @@
  *
  * Errors: 0 on success, negative errno-style code otherwise; the reference
  * panics where these return TSW_EINVAL (tswap.rs:94,112,136).
- * tsw_last_error(ctx) gives the message of the last failure.
+ * tsw_last_error(ctx) gives the message of the last failure. A failed call
+ * leaves the context consistent: no goal stays registered against a partial
+ * table and no next hop stays queued for a K3 pass that did not run.
  * One context is single-threaded; separate contexts may live on separate
  * threads or devices.
+ *
+ * Hard limits where the reference (usize arithmetic, unbounded Vec/HashMap)
+ * would keep going — each returns an error code, never a wrong answer:
+ *   - grid: at most 2048 cells per side and 2^20 cells      (tsw_create -> NULL)
+ *   - BFS distances are u16: a goal whose farthest reachable cell is more than
+ *     65534 steps away fails K1 with TSW_EOVERFLOW (only possible on grids of
+ *     more than 65535 free cells, e.g. a serpentine 1024x1024 maze)
+ *   - exact A*: the LDS-heap kernels hand queries with g >= 2^15, f >= 2^17 or
+ *     a heap past their LDS capacity to the global-heap kernel (20-bit g, enough
+ *     for any path on a 2^20-cell grid); its heap holds min(4*cells+8, 65536)
+ *     entries, past that TSW_EOVERFLOW
+ *   - tsw_decide: at most 1024 entries in one agent's nearby list (TSW_EOVERFLOW;
+ *     get_nearby, decentralized/agent.rs:108-153, has no bound)
+ *   - goal tables: table_budget_bytes (3 B per cell per goal). Tables not used by
+ *     the current call are evicted least-recently-used first; TSW_ENOMEM only
+ *     when the goals of ONE call do not fit.
+ *
+ * Device-memory arguments (*_device entry points) may be produced on any stream
+ * of the caller: the library synchronises the device before reading or writing
+ * them, and the call has completed its device work when it returns.
  */
 #ifndef TSWAP_H
 #define TSWAP_H
@@ -171,6 +193,7 @@ typedef struct {
     /* plan-kernel exits for K3 next-hop resolution, by the section that needed the codes
      * (same indices as plan_section_ms; [7] = relaunch entry) */
     uint64_t plan_exits[8];
+    uint64_t table_evictions;   /* goal tables dropped by the LRU (table_budget_bytes reached) */
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

@@ -87,7 +87,7 @@ class Stats(ctypes.Structure):
         ("assign_launches", ctypes.c_uint64), ("assign_ms", ctypes.c_double),
         ("steps", ctypes.c_uint64), ("tables", ctypes.c_uint64), ("plan_ms", ctypes.c_double),
         ("plan_section_ms", ctypes.c_double * 8), ("rule_rounds", ctypes.c_uint64),
-        ("plan_exits", ctypes.c_uint64 * 8),
+        ("plan_exits", ctypes.c_uint64 * 8), ("table_evictions", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -337,6 +337,11 @@ def tswap_mapd(grid, initial_positions, tasks, max_t: int = 2000):
 
 
 def tswap_step(grid, agents_v, agents_g):
-    """One `tswap_step` over cell ids (y*w+x), as the centralized manager calls it per tick."""
+    """One `tswap_step` over cell ids (y*w+x) on a throw-away context (tests, one-off calls).
+
+    For the centralized manager's per-tick use (plan_all_paths, bin/centralized/manager.rs:101-144)
+    keep ONE `Planner` for the grid and call `Planner.step` every tick: its goal tables and resolved
+    next hops persist across ticks (LRU-bounded by table_budget_bytes), where this function rebuilds
+    the context — grid upload, BFS tables, A* scratch — on every call."""
     with Planner(grid) as p:
         return p.step(np.asarray(agents_v), np.asarray(agents_g))

@@ -43,6 +43,55 @@ struct DevStatus {
 
 enum { CAT_BFS = 0, CAT_ASTAR = 1, CAT_WALK = 2, CAT_ASSIGN = 3, NCAT = 4 };
 
+// Diagnostic / A-B knobs. Read ONCE from the environment when the context is created (never on a
+// call path), so a context's behaviour cannot change under it. None changes a result: every
+// setting is covered by a bit-exact test. Defaults are the production configuration.
+struct Tunables {
+  uint32_t bfs_mode = 0;          // TSW_BFS_KERNEL: 0 auto, 1 wave (row words), 2 block, 3 blk (8x8), 4 big
+  uint32_t bfs_cap = 512;         // TSW_BFS_LISTCAP: k_bfs_wave LDS list entries
+  uint32_t blk_cap = 576;         // TSW_BFS_BLKCAP: k_bfs_blk LDS list entries
+  uint32_t bfs_waves = 16;        // TSW_BFS_WAVES: waves per K1 workgroup cap
+  bool bfs_order = true;          // TSW_BFS_ORDER=0: keep the caller's goal order (no LPT)
+  bool bfs_prof = false;          // TSW_BFS_PROF: print K1 cycle split per launch
+  uint32_t wave_hcap = 0;         // TSW_ASTAR_WAVE_HCAP: k_astar_wave LDS heap entries (0 = default)
+  int astar_global_gs = -1;       // TSW_ASTAR_GLOBAL_GS: -1 auto, 0 LDS g-scores, 1 global slots
+  bool astar_tier2 = true;        // TSW_ASTAR_NO_TIER2: skip the LDS-heap/global-g second tier
+  uint32_t astar_diag = 0;        // TSW_ASTAR_SERIAL / TSW_ASTAR_PROF (ASTAR_DIAG_*)
+  bool prefetch = true;           // TSW_NO_PREFETCH: no speculative next-hop prefetch
+  uint32_t wave_rules_max = 0xFFFFFFFFu;  // TSW_WAVE_RULES_MAX: wave-0 rules rounds when n <= this
+  uint32_t wide_prefetch = 8;     // TSW_WIDE_PREFETCH: resolved hops walked ahead (0 = candidates only)
+  bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
+  uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
+  bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
+
+  static Tunables from_env() {
+    Tunables t;
+    auto num = [](const char* k, long lo, long hi, long def) -> long {
+      const char* v = getenv(k);
+      if (!v) return def;
+      return std::max(lo, std::min(hi, atol(v)));
+    };
+    if (const char* m = getenv("TSW_BFS_KERNEL"))
+      t.bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : !strcmp(m, "blk") ? 3u : !strcmp(m, "big") ? 4u : 0u;
+    t.bfs_cap = (uint32_t)num("TSW_BFS_LISTCAP", 1, 32768, t.bfs_cap);
+    t.blk_cap = (uint32_t)num("TSW_BFS_BLKCAP", 1, 32768, t.blk_cap);
+    t.bfs_waves = (uint32_t)num("TSW_BFS_WAVES", 1, 16, t.bfs_waves);
+    t.bfs_order = num("TSW_BFS_ORDER", 0, 1, 1) != 0;
+    t.bfs_prof = getenv("TSW_BFS_PROF") != nullptr;
+    t.wave_hcap = (uint32_t)num("TSW_ASTAR_WAVE_HCAP", 4, 1 << 20, 0);
+    t.astar_global_gs = (int)num("TSW_ASTAR_GLOBAL_GS", 0, 1, -1);
+    t.astar_tier2 = getenv("TSW_ASTAR_NO_TIER2") == nullptr;
+    t.astar_diag = (getenv("TSW_ASTAR_SERIAL") ? ASTAR_DIAG_SERIAL : 0u) | (getenv("TSW_ASTAR_PROF") ? ASTAR_DIAG_PROF : 0u);
+    t.prefetch = getenv("TSW_NO_PREFETCH") == nullptr;
+    t.wave_rules_max = (uint32_t)num("TSW_WAVE_RULES_MAX", 0, 0xFFFFFFFFl, t.wave_rules_max);
+    t.wide_prefetch = (uint32_t)num("TSW_WIDE_PREFETCH", 0, 1 << 16, t.wide_prefetch);
+    t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
+    t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
+    t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
+    return t;
+  }
+};
+
 }  // namespace
 
 struct tsw_ctx {
@@ -50,16 +99,17 @@ struct tsw_ctx {
   hipStream_t s = nullptr;
   std::string err;
   uint32_t flags = 0;
+  Tunables tun;
   DevGrid G{};
   std::vector<uint8_t> h_nbmask;
   uint8_t* d_nbmask = nullptr;
   uint32_t* d_freebits = nullptr;
   int max_lds = 65536, num_cu = 256;
   // K1 v2 (k_bfs_wave) padded grid + per-wave scratch
-  uint32_t Wp = 0, npw = 0, bfs_cap = 512, bfs_mode = 0;  // mode 0 auto, 1 wave, 2 block, 3 blk8
+  uint32_t Wp = 0, npw = 0;
   uint32_t* d_frp = nullptr;
   // K1 v3 (k_bfs_blk) 8x8-block grid
-  uint32_t BW = 0, BH = 0, Bp = 0, nbp = 0, blk_cap = 576;
+  uint32_t BW = 0, BH = 0, Bp = 0, nbp = 0;
   uint64_t* d_frb = nullptr;
   uint32_t* d_abase = nullptr;  // k_bfs_blk run-start numbering
   uint32_t nrs = 0;
@@ -71,15 +121,20 @@ struct tsw_ctx {
   size_t scratch_words = 0, scratch_lwords = 0;
   unsigned long long* d_bprof = nullptr;  // TSW_BFS_PROF=1: k_bfs_wave cycle split, printed per launch
 
-  // goal-table store
+  // goal-table store: slots 0 .. tab_count-1 have been handed out at least once; a slot is live
+  // iff h_tab_goal[slot] != NO_GOAL. Slots of evicted tables sit on tab_free for reuse.
   uint64_t tstride = 0;
-  uint32_t tab_cap = 0, tab_count = 0;
+  uint32_t tab_cap = 0, tab_count = 0, tab_live = 0;
   uint16_t* d_dist = nullptr;
   uint8_t* d_nh = nullptr;
   int32_t* d_goal_tab = nullptr;
   std::vector<int32_t> h_goal_tab;
   std::vector<uint32_t> h_tab_goal;
+  std::vector<uint64_t> h_tab_stamp;  // call counter of the slot's last use (LRU eviction)
+  std::vector<uint32_t> tab_free;
+  uint64_t call_stamp = 0;
   uint64_t table_budget = 0;
+  uint64_t evictions = 0;
 
   // A* scratch
   uint32_t nslots = 0, hcap = 0;
@@ -87,7 +142,6 @@ struct tsw_ctx {
   uint32_t* d_gs = nullptr;
   uint32_t* d_epochs = nullptr;
   uint32_t nslots16 = 0;  // LDS-heap A* (small grids)
-  uint32_t wave_hcap = 0;  // k_astar_wave LDS heap entries (0: default; TSW_ASTAR_WAVE_HCAP, tests)
   uint16_t* d_gs16 = nullptr;
   uint32_t* d_ep16 = nullptr;
   AstarQuery* d_ovf = nullptr;
@@ -273,8 +327,7 @@ int ensure_tmp(tsw_ctx* c, size_t k) {
 // otherwise idle chip. Output positions are carried in `slots`. TSW_BFS_ORDER=0 keeps the
 // caller's order (A/B).
 void bfs_lpt_order(const tsw_ctx* c, std::vector<uint32_t>& goals, std::vector<uint32_t>& slots) {
-  static const bool off = getenv("TSW_BFS_ORDER") && atoi(getenv("TSW_BFS_ORDER")) == 0;
-  if (off || goals.size() < 2) return;
+  if (!c->tun.bfs_order || goals.size() < 2) return;
   const uint32_t W = c->G.W, H = c->G.H, maxe = W + H;
   // counting sort by eccentricity bound, descending, stable: O(k + W + H) on the host
   std::vector<uint32_t> cnt(maxe + 1u, 0u), ecc(goals.size());
@@ -396,22 +449,23 @@ int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint
     // the heap in LDS and the g_scores in the global slots (3-4 waves per CU; wh10k prefix
     // 3.32 -> 2.68 s); a smaller batch is bound by its slowest query, where LDS g_scores are
     // faster per pop. TSW_ASTAR_GLOBAL_GS=0/1 forces either (A/B).
-    const char* ge = getenv("TSW_ASTAR_GLOBAL_GS");
-    const bool ggs = ge ? atoi(ge) != 0
-                        : astar_wave_lds_gs(c->G) && nq > std::min(astar_wave_slots(c->G, c->num_cu), c->nslots);
+    const int ge = c->tun.astar_global_gs;
+    const bool ggs = ge >= 0 ? ge != 0
+                             : astar_wave_lds_gs(c->G) && nq > std::min(astar_wave_slots(c->G, c->num_cu), c->nslots);
     const uint32_t slots = std::min(astar_wave_slots(c->G, c->num_cu, ggs), c->nslots);
     HIPCHK(launch_astar_wave(c->G, Q, nq, nh, c->tstride, res, lens, c->d_gs, c->d_epochs, slots, c->d_ovf,
-                             &c->d_stat->novf, c->wave_hcap, ggs, c->s, &c->d_stat->qnext));
+                             &c->d_stat->novf, c->tun.wave_hcap, ggs, c->s, &c->d_stat->qnext, c->tun.astar_diag));
     HIPCHK(hipMemcpyAsync(&c->h_stat->novf, &c->d_stat->novf, 4, hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     uint32_t novf = c->h_stat->novf;
     AstarQuery* rest = c->d_ovf;
-    if (novf && astar_wave_lds_gs(c->G) && !getenv("TSW_ASTAR_NO_TIER2")) {
+    if (novf && astar_wave_lds_gs(c->G) && c->tun.astar_tier2) {
       // second tier: g_scores that outgrew the LDS encoding (byte words: detours > 62) move to
       // the global u32 slots while the heap stays in LDS; only heap overflows reach k_astar
       const uint32_t slots2 = std::min(astar_wave_slots(c->G, c->num_cu, true), c->nslots);
       HIPCHK(launch_astar_wave(c->G, c->d_ovf, novf, nh, c->tstride, res, lens, c->d_gs, c->d_epochs, slots2,
-                               c->d_ovf2, &c->d_stat->novf2, c->wave_hcap, true, c->s, &c->d_stat->qnext2));
+                               c->d_ovf2, &c->d_stat->novf2, c->tun.wave_hcap, true, c->s, &c->d_stat->qnext2,
+                               c->tun.astar_diag));
       HIPCHK(hipMemcpyAsync(&c->h_stat->novf2, &c->d_stat->novf2, 4, hipMemcpyDeviceToHost, c->s));
       HIPCHK(hipStreamSynchronize(c->s));
       novf = c->h_stat->novf2;
@@ -426,7 +480,18 @@ int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint
   return TSW_OK;
 }
 
-int resolve_all_unknown(tsw_ctx* c, const std::vector<uint32_t>& goals, const std::vector<uint32_t>& slots) {
+// Error path after pairs were marked NH_PENDING (queued for a K3 pass that did not complete):
+// put every pending code of the store back to NH_UNKNOWN so later calls re-queue them instead of
+// waiting on a pass that will never run. Returns rc (the original failure).
+int reset_pending_after(tsw_ctx* c, int rc) {
+  if (rc == TSW_OK || !c->d_nh || c->tab_count == 0) return rc;
+  (void)hipStreamSynchronize(c->s);
+  if (launch_reset_pending(c->d_nh, (uint64_t)c->tab_count * c->tstride, c->s) == hipSuccess)
+    (void)hipStreamSynchronize(c->s);
+  return rc;
+}
+
+int resolve_all_unknown_impl(tsw_ctx* c, const std::vector<uint32_t>& goals, const std::vector<uint32_t>& slots) {
   if (goals.empty()) return TSW_OK;
   TRY(ensure_astar_scratch(c));
   TRY(ensure_tmp(c, goals.size()));
@@ -451,6 +516,10 @@ int resolve_all_unknown(tsw_ctx* c, const std::vector<uint32_t>& goals, const st
     if (cnt <= c->qcap) break;
   }
   return TSW_OK;
+}
+
+int resolve_all_unknown(tsw_ctx* c, const std::vector<uint32_t>& goals, const std::vector<uint32_t>& slots) {
+  return reset_pending_after(c, resolve_all_unknown_impl(c, goals, slots));
 }
 
 bool eager_policy(const tsw_ctx* c, size_t new_tables) {
@@ -483,7 +552,7 @@ int ensure_wave_scratch(tsw_ctx* c, uint64_t want, size_t words, size_t lwords) 
 }
 
 unsigned long long* bfs_prof_buf(tsw_ctx* c) {
-  if (!getenv("TSW_BFS_PROF")) return nullptr;
+  if (!c->tun.bfs_prof) return nullptr;
   if (!c->d_bprof && hipMalloc(&c->d_bprof, 4 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
   if (hipMemsetAsync(c->d_bprof, 0, 4 * sizeof(unsigned long long), c->s) != hipSuccess) return nullptr;
   return c->d_bprof;
@@ -506,11 +575,12 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
             uint8_t* nh) {
   if (k == 0) return TSW_OK;
   const bool vec16 = c->G.W % 8u == 0u && dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u;
-  const uint32_t max_waves = getenv("TSW_BFS_WAVES") ? (uint32_t)std::max(1, atoi(getenv("TSW_BFS_WAVES"))) : 16u;
+  const uint32_t max_waves = c->tun.bfs_waves;
+  const uint32_t bfs_mode = c->tun.bfs_mode;
   uint32_t nbw = 0;
-  if ((c->bfs_mode == 0 || c->bfs_mode == 3) && c->nbp <= 0x10000u)
-    nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->blk_cap, c->max_lds));
-  if (nbw == 0 && c->bfs_mode == 3) RET(TSW_EINVAL, "k_bfs_blk does not fit this grid (TSW_BFS_KERNEL=blk)");
+  if ((bfs_mode == 0 || bfs_mode == 3) && c->nbp <= 0x10000u)
+    nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->tun.blk_cap, c->max_lds));
+  if (nbw == 0 && bfs_mode == 3) RET(TSW_EINVAL, "k_bfs_blk does not fit this grid (TSW_BFS_KERNEL=blk)");
   if (nbw > 0) {
     Timer t(c, CAT_BFS);
     TRY(ensure_wave_scratch(c, (uint64_t)c->num_cu * nbw, std::max<size_t>(c->nrs, 1), (size_t)c->nbp * 2u));
@@ -529,7 +599,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     A.BH = c->BH;
     A.Bp = c->Bp;
     A.nbp = c->nbp;
-    A.cap = c->blk_cap;
+    A.cap = c->tun.blk_cap;
     A.frb = c->d_frb;
     A.abase = c->d_abase;
     A.nrs = c->nrs;
@@ -554,9 +624,52 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     return TSW_OK;
   }
   uint32_t nwv = 0;
-  if ((c->bfs_mode == 0 || c->bfs_mode == 1) && c->npw <= 0x8000u)
-    nwv = bfs_wave_waves_per_block(c->npw, c->bfs_cap, c->max_lds);
-  if (nwv == 0 && c->bfs_mode == 1) RET(TSW_EINVAL, "k_bfs_wave does not fit this grid (TSW_BFS_KERNEL=wave)");
+  if ((bfs_mode == 0 || bfs_mode == 1) && c->npw <= 0x8000u)
+    nwv = bfs_wave_waves_per_block(c->npw, c->tun.bfs_cap, c->max_lds);
+  if (nwv == 0 && bfs_mode == 1) RET(TSW_EINVAL, "k_bfs_wave does not fit this grid (TSW_BFS_KERNEL=wave)");
+  uint32_t big_cap = 0;
+  if (nwv == 0 && (bfs_mode == 0 || bfs_mode == 4) && bfs_big_fits(c->nbp, c->max_lds, &big_cap)) {
+    // large grids (e.g. 1024x1024): one workgroup per goal, shared visited bitmap in LDS
+    Timer t(c, CAT_BFS);
+    const uint32_t nwg = bfs_big_workgroups(c->nbp, big_cap, c->num_cu);
+    TRY(ensure_wave_scratch(c, nwg, std::max<size_t>(c->nrs, 1), (size_t)c->nbp * 2u));
+    if (c->wlg_waves < c->wave_scratch) {
+      HIPCHK(hipStreamSynchronize(c->s));
+      if (c->d_wlg) HIPCHK(hipFree(c->d_wlg));
+      c->d_wlg = nullptr;
+      c->wlg_waves = 0;
+      HIPCHK(hipMalloc(&c->d_wlg, (size_t)c->wave_scratch * c->nbp * 8u));
+      c->wlg_waves = c->wave_scratch;
+    }
+    BigBfsArgs A{};
+    A.W = c->G.W;
+    A.H = c->G.H;
+    A.BW = c->BW;
+    A.BH = c->BH;
+    A.Bp = c->Bp;
+    A.nbp = c->nbp;
+    A.cap = big_cap;
+    A.frb = c->d_frb;
+    A.abase = c->d_abase;
+    A.goals = goals;
+    A.slots = slots;
+    A.k = k;
+    A.dist = dist;
+    A.dstride = dstride;
+    A.nrs = std::max<uint32_t>(c->nrs, 1u);
+    A.anch = c->d_anch;
+    A.lovf = c->d_lovf;
+    A.wlg = reinterpret_cast<uint64_t*>(c->d_wlg);
+    A.work = &c->d_stat->work;
+    A.err = &c->d_stat->err;
+    A.vec16 = vec16 ? 1u : 0u;
+    A.scratch_wgs = (uint32_t)std::min<uint64_t>(c->wave_scratch, c->wlg_waves);
+    HIPCHK(hipMemsetAsync(&c->d_stat->work, 0, 4, c->s));
+    HIPCHK(launch_bfs_big(A, c->max_lds, c->num_cu, c->s));
+    if (nh) HIPCHK(launch_classify(c->G, goals, slots, k, dist, dstride, nh, c->s));
+    return TSW_OK;
+  }
+  if (bfs_mode == 4) RET(TSW_EINVAL, "k_bfs_big does not fit this grid (TSW_BFS_KERNEL=big)");
   Timer t(c, CAT_BFS);
   if (nwv == 0) {
     HIPCHK(launch_bfs(c->G, goals, slots, k, dist, dstride, nh, dstride, &c->d_stat->err, c->max_lds, c->num_cu,
@@ -570,7 +683,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   A.Ww = c->G.Ww;
   A.Wp = c->Wp;
   A.npw = c->npw;
-  A.cap = c->bfs_cap;
+  A.cap = c->tun.bfs_cap;
   A.frp = c->d_frp;
   A.goals = goals;
   A.slots = slots;
@@ -592,50 +705,125 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   return TSW_OK;
 }
 
-// Make sure every goal in `goals` (valid free cells) has a table.
-int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
-  std::vector<uint32_t> newg;
-  newg.reserve(goals_in.size());
-  for (uint32_t g : goals_in)
-    if (c->h_goal_tab[g] == -1) {
-      c->h_goal_tab[g] = -2;  // mark (dedupe)
-      newg.push_back(g);
-    }
-  if (newg.empty()) return TSW_OK;
-  const size_t need = (size_t)c->tab_count + newg.size();
-  const uint64_t per_tab = c->tstride * 3ull;
-  if (need > c->tab_cap) {
-    size_t nc = std::max<size_t>(need, std::max<size_t>((size_t)c->tab_cap * 2, 64));
-    const uint64_t max_tabs = c->table_budget / per_tab;
-    if (nc > max_tabs) nc = std::max<size_t>(need, (size_t)max_tabs);
-    if ((uint64_t)need > max_tabs) {
-      for (uint32_t g : newg) c->h_goal_tab[g] = -1;
-      RET(TSW_ENOMEM, "goal-table budget exceeded (raise tsw_opts.table_budget_bytes)");
-    }
+constexpr uint32_t NO_GOAL = 0xFFFFFFFFu;
+
+// Grow the device store to at least `need` slots (never past the budget; callers check).
+int grow_store(tsw_ctx* c, size_t need) {
+  if (need <= c->tab_cap) return TSW_OK;
+  const uint64_t max_tabs = c->table_budget / (c->tstride * 3ull);
+  size_t nc = std::max<size_t>(need, std::max<size_t>((size_t)c->tab_cap * 2, 64));
+  nc = std::max<size_t>(need, std::min<size_t>(nc, (size_t)max_tabs));
+  HIPCHK(hipStreamSynchronize(c->s));
+  uint16_t* nd = nullptr;
+  uint8_t* nn = nullptr;
+  HIPCHK(hipMalloc(&nd, nc * c->tstride * 2ull));
+  if (hipError_t e = hipMalloc(&nn, nc * c->tstride); e != hipSuccess) {
+    (void)hipFree(nd);
+    RET(TSW_ENOMEM, std::string("table store growth: ") + hipGetErrorString(e));
+  }
+  if (c->tab_count) {
+    HIPCHK(hipMemcpyAsync(nd, c->d_dist, (size_t)c->tab_count * c->tstride * 2ull, hipMemcpyDeviceToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(nn, c->d_nh, (size_t)c->tab_count * c->tstride, hipMemcpyDeviceToDevice, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
-    uint16_t* nd = nullptr;
-    uint8_t* nn = nullptr;
-    HIPCHK(hipMalloc(&nd, nc * c->tstride * 2ull));
-    HIPCHK(hipMalloc(&nn, nc * c->tstride));
-    if (c->tab_count) {
-      HIPCHK(hipMemcpyAsync(nd, c->d_dist, (size_t)c->tab_count * c->tstride * 2ull, hipMemcpyDeviceToDevice, c->s));
-      HIPCHK(hipMemcpyAsync(nn, c->d_nh, (size_t)c->tab_count * c->tstride, hipMemcpyDeviceToDevice, c->s));
-      HIPCHK(hipStreamSynchronize(c->s));
+  }
+  if (c->d_dist) HIPCHK(hipFree(c->d_dist));
+  if (c->d_nh) HIPCHK(hipFree(c->d_nh));
+  c->d_dist = nd;
+  c->d_nh = nn;
+  c->tab_cap = (uint32_t)nc;
+  c->h_tab_goal.resize(nc, NO_GOAL);
+  c->h_tab_stamp.resize(nc, 0);
+  return TSW_OK;
+}
+
+// Stamp the tables of `goals` as used by the current call and collect the goals that have none
+// (deduplicated, marked -2 in h_goal_tab until committed or rolled back).
+void stamp_and_collect(tsw_ctx* c, const uint32_t* goals, size_t k, std::vector<uint32_t>& newg,
+                       std::vector<uint32_t>* src = nullptr) {
+  ++c->call_stamp;
+  for (size_t i = 0; i < k; ++i) {
+    const uint32_t g = goals[i];
+    const int32_t t = c->h_goal_tab[g];
+    if (t >= 0) {
+      c->h_tab_stamp[t] = c->call_stamp;
+    } else if (t == -1) {
+      c->h_goal_tab[g] = -2;
+      newg.push_back(g);
+      if (src) src->push_back((uint32_t)i);
     }
-    if (c->d_dist) HIPCHK(hipFree(c->d_dist));
-    if (c->d_nh) HIPCHK(hipFree(c->d_nh));
-    c->d_dist = nd;
-    c->d_nh = nn;
-    c->tab_cap = (uint32_t)nc;
-    c->h_tab_goal.resize(nc, 0);
   }
-  std::vector<uint32_t> slots(newg.size());
-  for (size_t k = 0; k < newg.size(); ++k) {
-    slots[k] = c->tab_count + (uint32_t)k;
-    c->h_goal_tab[newg[k]] = (int32_t)slots[k];
-    c->h_tab_goal[slots[k]] = newg[k];
+}
+
+// Slots for k new tables: free slots first, then growth up to the budget, then the least-recently
+// used live tables that the current call does not use (LRU eviction — a long-running per-tick
+// manager streams goals through a bounded store instead of failing, SURVEY §7 hard part 4).
+// Evicted goals lose their table (goal_tab -1); later calls rebuild them on demand.
+int reserve_slots(tsw_ctx* c, size_t k, std::vector<uint32_t>& slots) {
+  slots.clear();
+  const uint64_t max_tabs = c->table_budget / (c->tstride * 3ull);
+  while (slots.size() < k && !c->tab_free.empty()) {
+    slots.push_back(c->tab_free.back());
+    c->tab_free.pop_back();
   }
-  c->tab_count = (uint32_t)need;
+  size_t want = k - slots.size();
+  const size_t fresh = std::min<size_t>(want, max_tabs > c->tab_count ? (size_t)(max_tabs - c->tab_count) : 0u);
+  if (fresh) {
+    if (int r = grow_store(c, (size_t)c->tab_count + fresh); r != TSW_OK) {
+      c->tab_free.insert(c->tab_free.end(), slots.begin(), slots.end());
+      slots.clear();
+      return r;
+    }
+    for (size_t j = 0; j < fresh; ++j) slots.push_back(c->tab_count++);
+    want -= fresh;
+  }
+  if (want) {
+    std::vector<uint32_t> cand;
+    for (uint32_t s = 0; s < c->tab_count; ++s)
+      if (c->h_tab_goal[s] != NO_GOAL && c->h_tab_stamp[s] < c->call_stamp) cand.push_back(s);
+    if (cand.size() < want) {
+      c->tab_free.insert(c->tab_free.end(), slots.begin(), slots.end());
+      slots.clear();
+      RET(TSW_ENOMEM, "goal-table budget exceeded by the goals of one call (raise tsw_opts.table_budget_bytes)");
+    }
+    std::partial_sort(cand.begin(), cand.begin() + want, cand.end(),
+                      [&](uint32_t a, uint32_t b) { return c->h_tab_stamp[a] < c->h_tab_stamp[b]; });
+    for (size_t j = 0; j < want; ++j) {
+      const uint32_t s = cand[j];
+      c->h_goal_tab[c->h_tab_goal[s]] = -1;
+      c->h_tab_goal[s] = NO_GOAL;
+      --c->tab_live;
+      ++c->evictions;
+      slots.push_back(s);
+    }
+  }
+  return TSW_OK;
+}
+
+// Commit (rc == OK) or roll back the new goals and their reserved slots, then publish goal_tab.
+int finish_tables(tsw_ctx* c, int rc, const std::vector<uint32_t>& newg, const std::vector<uint32_t>& slots) {
+  for (size_t j = 0; j < newg.size(); ++j) {
+    if (rc == TSW_OK && j < slots.size()) {
+      c->h_goal_tab[newg[j]] = (int32_t)slots[j];
+      c->h_tab_goal[slots[j]] = newg[j];
+      c->h_tab_stamp[slots[j]] = c->call_stamp;
+    } else {
+      c->h_goal_tab[newg[j]] = -1;
+    }
+  }
+  if (rc == TSW_OK) c->tab_live += (uint32_t)newg.size();
+  else c->tab_free.insert(c->tab_free.end(), slots.begin(), slots.end());
+  c->st.tables = c->tab_live;
+  const std::string keep = c->err;
+  if (hipMemcpyAsync(c->d_goal_tab, c->h_goal_tab.data(), (size_t)c->G.ncell * 4, hipMemcpyHostToDevice, c->s) !=
+          hipSuccess ||
+      hipStreamSynchronize(c->s) != hipSuccess) {
+    if (rc == TSW_OK) RET(TSW_EHIP, "goal_tab upload failed");
+  }
+  c->err = keep;
+  return rc;
+}
+
+int build_new_tables(tsw_ctx* c, const std::vector<uint32_t>& newg, const std::vector<uint32_t>& slots) {
   std::vector<uint32_t>& lg = c->h_lpt_goals;
   std::vector<uint32_t>& ls = c->h_lpt_slots;
   lg = newg;
@@ -647,9 +835,19 @@ int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
   TRY(run_bfs(c, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh));
   c->st.bfs_goals += newg.size();
   c->st.bfs_launches++;
-  HIPCHK(hipMemcpyAsync(c->d_goal_tab, c->h_goal_tab.data(), (size_t)c->G.ncell * 4, hipMemcpyHostToDevice, c->s));
-  TRY(check_err(c));
-  c->st.tables = c->tab_count;
+  return check_err(c);
+}
+
+// Make sure every goal in `goals` (valid free cells) has a table. A failed K1 build (HIP error,
+// distance overflow) leaves no goal registered against a partial table.
+int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
+  std::vector<uint32_t> newg, slots;
+  newg.reserve(goals_in.size());
+  stamp_and_collect(c, goals_in.data(), goals_in.size(), newg);
+  if (newg.empty()) return TSW_OK;
+  int rc = reserve_slots(c, newg.size(), slots);
+  if (rc == TSW_OK) rc = build_new_tables(c, newg, slots);
+  TRY(finish_tables(c, rc, newg, slots));
   if (eager_policy(c, newg.size())) TRY(resolve_all_unknown(c, newg, slots));
   return TSW_OK;
 }
@@ -712,14 +910,14 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.mu = c->d_mu;
   P.has_dups = *c->h_dups;
   // speculative next-hop prefetch only pays in lazy mode (eager tables have nothing unresolved)
-  P.prefetch = (getenv("TSW_NO_PREFETCH") || eager_policy(c, 0)) ? 0u : 1u;
+  P.prefetch = (!c->tun.prefetch || eager_policy(c, 0)) ? 0u : 1u;
   // wide prefetch (default 8 hops; 4 -> 8: wh10k prefix 2.53 -> 2.28 s, 16 gave 2.32 s): every
   // agent's (succ cell, goal) pair, and its path walked this many hops ahead; TSW_WIDE_PREFETCH=0 restores candidates-only / one hop (A/B)
   // wave-0 rules rounds (scan 64 agents per ballot from the cursor, fire in lane 0): firing
   // agents are dense, so a scan rarely needs more than a chunk or two even for 10k agents;
   // TSW_WAVE_RULES_MAX caps n for A/B
-  P.wave_rules_max = getenv("TSW_WAVE_RULES_MAX") ? (uint32_t)std::max(0, atoi(getenv("TSW_WAVE_RULES_MAX"))) : 0xFFFFFFFFu;
-  P.wide_prefetch = getenv("TSW_WIDE_PREFETCH") ? (uint32_t)std::max(0, atoi(getenv("TSW_WIDE_PREFETCH"))) : 8u;
+  P.wave_rules_max = c->tun.wave_rules_max;
+  P.wide_prefetch = c->tun.wide_prefetch;
   P.pick_xy = c->d_pick_xy;
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;
@@ -733,12 +931,12 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.grec = want_goals ? c->d_grec : nullptr;
   P.ctl = c->d_ctl;
   P.sec_ticks = c->d_ticks;
-  P.dbg = getenv("TSW_PLAN_DEBUG") ? 1u : 0u;
+  P.dbg = c->tun.plan_debug ? 1u : 0u;
   // LDS residency, in priority order: agents, occupancy grid, task table
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
   // without the agent arrays, the rules relabel's pointer-doubling buffers come next
-  bool fl = !ag && !getenv("TSW_NO_FLINKS_LDS") && plan_lds_bytes(n, P.ncell, m, false, false, false, true) <= budget;
+  bool fl = !ag && c->tun.flinks_lds && plan_lds_bytes(n, P.ncell, m, false, false, false, true) <= budget;
   bool oc = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl) <= budget;
   bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl) <= budget;
   P.f_lds = fl;
@@ -758,13 +956,13 @@ int build_occ(tsw_ctx* c, uint32_t n) {
 }
 
 // Drive k_plan until it reports done; each NEED_QUERIES exit runs K3 on the queued pairs.
-int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
+int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   *c->h_ctl = init;
   HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
   const size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds);
   // one lane per agent in the parallel passes when possible; >= 4 waves for the task argmin
   uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
-  if (const char* e = getenv("TSW_PLAN_BLOCK")) block = (uint32_t)std::max(64, std::min(atoi(e), 1024)) / 64u * 64u;
+  if (c->tun.plan_block) block = std::max<uint32_t>(64u, c->tun.plan_block);
   for (uint64_t round = 0;; ++round) {
     if (round > 16ull * P.n + 4096ull * (init.max_t + 1)) RET(TSW_EINVAL, "plan kernel made no progress");
     {
@@ -783,7 +981,7 @@ int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     if (k.status == PLAN_DONE) {
       c->chase_id = k.chase_id;
       c->st.rule_rounds += k.rule_rounds;
-      if (getenv("TSW_PLAN_DEBUG")) {
+      if (c->tun.plan_debug) {
         unsigned long long tk[16];
         HIPCHK(hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost));
         fprintf(stderr, "[k_plan] steps %u rule rounds %u move rounds %u launches %llu | move A-E us %.0f %.0f %.0f %.0f %.0f"
@@ -806,6 +1004,11 @@ int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
     TRY(check_err(c));
   }
+}
+
+// Any failure after k_plan queued pairs leaves their codes PENDING: reset them.
+int run_plan(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
+  return reset_pending_after(c, run_plan_impl(c, P, init));
 }
 
 int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* tasks, uint32_t m,
@@ -924,6 +1127,7 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
     return nullptr;
   }
   tsw_ctx* c = new tsw_ctx();
+  c->tun = Tunables::from_env();  // the only place the environment is read
   c->device = opts ? opts->device : 0;
   c->flags = opts ? opts->flags : 0;
   if (c->device < 0 || c->device >= ndev) {
@@ -1017,11 +1221,6 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
     if ((e = hipMalloc(&c->d_frb, (size_t)c->nbp * 8)) != hipSuccess) return fail("malloc frb", e);
     if ((e = hipMemcpy(c->d_frb, frb.data(), (size_t)c->nbp * 8, hipMemcpyHostToDevice)) != hipSuccess)
       return fail("copy frb", e);
-    if (const char* m = getenv("TSW_BFS_KERNEL"))
-      c->bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : !strcmp(m, "blk") ? 3u : 0u;
-    if (const char* m = getenv("TSW_BFS_LISTCAP")) c->bfs_cap = std::max(1, std::min(atoi(m), 32768));
-    if (const char* m = getenv("TSW_ASTAR_WAVE_HCAP")) c->wave_hcap = (uint32_t)std::max(4, atoi(m));
-    if (const char* m = getenv("TSW_BFS_BLKCAP")) c->blk_cap = std::max(1, std::min(atoi(m), 32768));
   }
   c->h_goal_tab.assign(ncell, -1);
   if ((e = hipMalloc(&c->d_goal_tab, (size_t)ncell * 4)) != hipSuccess) return fail("malloc goal_tab", e);
@@ -1117,9 +1316,9 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   return TSW_OK;
 }
 
-int tsw_decide(tsw_ctx* c, const uint32_t* my_v, const uint32_t* my_g, uint32_t n, const uint32_t* nb_off,
-               const uint32_t* nb_v, const uint32_t* nb_g, uint32_t* act, uint32_t* cell, uint32_t* partner,
-               uint32_t* npart, uint32_t* part) {
+static int decide_impl(tsw_ctx* c, const uint32_t* my_v, const uint32_t* my_g, uint32_t n, const uint32_t* nb_off,
+                       const uint32_t* nb_v, const uint32_t* nb_g, uint32_t* act, uint32_t* cell, uint32_t* partner,
+                       uint32_t* npart, uint32_t* part) {
   if (!c) return TSW_EINVAL;
   if (n == 0) return TSW_OK;
   if (!my_v || !my_g || !nb_off || !act || !cell || !partner || !npart || !part) RET(TSW_EINVAL, "null argument");
@@ -1240,6 +1439,14 @@ int tsw_decide(tsw_ctx* c, const uint32_t* my_v, const uint32_t* my_g, uint32_t 
   return TSW_OK;
 }
 
+int tsw_decide(tsw_ctx* c, const uint32_t* my_v, const uint32_t* my_g, uint32_t n, const uint32_t* nb_off,
+               const uint32_t* nb_v, const uint32_t* nb_g, uint32_t* act, uint32_t* cell, uint32_t* partner,
+               uint32_t* npart, uint32_t* part) {
+  if (!c) return TSW_EINVAL;
+  // a failed round may leave queued pairs PENDING: reset them before returning the error
+  return reset_pending_after(c, decide_impl(c, my_v, my_g, n, nb_off, nb_v, nb_g, act, cell, partner, npart, part));
+}
+
 int tsw_get_path_next(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, uint32_t k, uint32_t* next,
                       int32_t* len) {
   if (!c) return TSW_EINVAL;
@@ -1317,6 +1524,9 @@ int tsw_dist_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16
   TRY(set_device(c));
   for (uint32_t i = 0; i < k; ++i)
     if (!cell_id_ok(c, goals[i])) RET(TSW_EINVAL, "goal cell off-grid or blocked");
+  // dev_out may have been allocated / zero-filled on another stream of the caller (e.g. torch's
+  // current stream): order every outstanding device work before writing into it
+  HIPCHK(hipDeviceSynchronize());
   TRY(ensure_tmp(c, k));
   // context-owned staging (like the caller's `goals`, read by the copy before it returns)
   std::vector<uint32_t>& lg = c->h_lpt_goals;
@@ -1340,60 +1550,30 @@ int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, cons
   if (k == 0) return TSW_OK;
   if (!goals || !dev_tables) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
-  std::vector<uint32_t> newg, src;
-  for (uint32_t i = 0; i < k; ++i) {
+  for (uint32_t i = 0; i < k; ++i)
     if (!cell_id_ok(c, goals[i])) RET(TSW_EINVAL, "goal cell off-grid or blocked");
-    if (c->h_goal_tab[goals[i]] == -1) {
-      c->h_goal_tab[goals[i]] = -2;
-      newg.push_back(goals[i]);
-      src.push_back(i);
-    }
-  }
-  for (uint32_t g : newg) c->h_goal_tab[g] = -1;
+  // the tables were produced on the caller's streams (e.g. an RCCL all-gather): complete first
+  HIPCHK(hipDeviceSynchronize());
+  std::vector<uint32_t> newg, src, slots;
+  stamp_and_collect(c, goals, k, newg, &src);
   if (newg.empty()) return TSW_OK;
-  const size_t need = (size_t)c->tab_count + newg.size();
-  if (need > c->tab_cap) {
-    // grow through ensure_tables' path by temporarily computing nothing: reuse its allocator
-    const uint64_t per_tab = c->tstride * 3ull;
-    size_t nc = std::max<size_t>(need, std::max<size_t>((size_t)c->tab_cap * 2, 64));
-    const uint64_t max_tabs = c->table_budget / per_tab;
-    if ((uint64_t)need > max_tabs) RET(TSW_ENOMEM, "goal-table budget exceeded");
-    nc = std::min<size_t>(nc, (size_t)max_tabs);
+  auto ingest = [&]() -> int {
+    TRY(reserve_slots(c, newg.size(), slots));
+    const size_t ncell = c->G.ncell;
+    for (size_t j = 0; j < newg.size(); ++j)
+      HIPCHK(hipMemcpyAsync(c->d_dist + (size_t)slots[j] * c->tstride, dev_tables + (size_t)src[j] * ncell,
+                            ncell * 2, hipMemcpyDeviceToDevice, c->s));
+    TRY(ensure_tmp(c, newg.size()));
+    HIPCHK(hipMemcpyAsync(c->d_tmp_a, newg.data(), newg.size() * 4, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
+    HIPCHK(launch_classify(c->G, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh,
+                           c->s));
     HIPCHK(hipStreamSynchronize(c->s));
-    uint16_t* nd = nullptr;
-    uint8_t* nn = nullptr;
-    HIPCHK(hipMalloc(&nd, nc * c->tstride * 2ull));
-    HIPCHK(hipMalloc(&nn, nc * c->tstride));
-    if (c->tab_count) {
-      HIPCHK(hipMemcpyAsync(nd, c->d_dist, (size_t)c->tab_count * c->tstride * 2ull, hipMemcpyDeviceToDevice, c->s));
-      HIPCHK(hipMemcpyAsync(nn, c->d_nh, (size_t)c->tab_count * c->tstride, hipMemcpyDeviceToDevice, c->s));
-      HIPCHK(hipStreamSynchronize(c->s));
-    }
-    if (c->d_dist) HIPCHK(hipFree(c->d_dist));
-    if (c->d_nh) HIPCHK(hipFree(c->d_nh));
-    c->d_dist = nd;
-    c->d_nh = nn;
-    c->tab_cap = (uint32_t)nc;
-    c->h_tab_goal.resize(nc, 0);
-  }
-  std::vector<uint32_t> slots(newg.size());
-  const size_t ncell = c->G.ncell;
-  for (size_t j = 0; j < newg.size(); ++j) {
-    slots[j] = c->tab_count + (uint32_t)j;
-    c->h_goal_tab[newg[j]] = (int32_t)slots[j];
-    c->h_tab_goal[slots[j]] = newg[j];
-    HIPCHK(hipMemcpyAsync(c->d_dist + (size_t)slots[j] * c->tstride, dev_tables + (size_t)src[j] * ncell, ncell * 2,
-                          hipMemcpyDeviceToDevice, c->s));
-  }
-  c->tab_count = (uint32_t)need;
-  TRY(ensure_tmp(c, newg.size()));
-  HIPCHK(hipMemcpyAsync(c->d_tmp_a, newg.data(), newg.size() * 4, hipMemcpyHostToDevice, c->s));
-  HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
-  HIPCHK(launch_classify(c->G, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh, c->s));
-  HIPCHK(hipMemcpyAsync(c->d_goal_tab, c->h_goal_tab.data(), ncell * 4, hipMemcpyHostToDevice, c->s));
-  HIPCHK(hipStreamSynchronize(c->s));
-  c->st.tables = c->tab_count;
+    return TSW_OK;
+  };
+  TRY(finish_tables(c, ingest(), newg, slots));
   if (eager_policy(c, newg.size())) TRY(resolve_all_unknown(c, newg, slots));
+  resolve_timing(c);
   return TSW_OK;
 }
 
@@ -1425,6 +1605,9 @@ int tsw_clear_tables(tsw_ctx* c) {
   HIPCHK(hipMemcpyAsync(c->d_goal_tab, c->h_goal_tab.data(), (size_t)c->G.ncell * 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipStreamSynchronize(c->s));
   c->tab_count = 0;
+  c->tab_live = 0;
+  c->tab_free.clear();
+  std::fill(c->h_tab_goal.begin(), c->h_tab_goal.end(), NO_GOAL);
   c->st.tables = 0;
   return TSW_OK;
 }
@@ -1437,6 +1620,8 @@ int tsw_get_stats(const tsw_ctx* c, tsw_stats* out) {
   if (hipSetDevice(c->device) == hipSuccess && hipStreamSynchronize(c->s) == hipSuccess)
     (void)hipMemcpy(ticks, c->d_ticks, sizeof ticks, hipMemcpyDeviceToHost);
   *out = c->st;
+  out->tables = c->tab_live;
+  out->table_evictions = c->evictions;
   for (int k = 0; k < 8; ++k) out->plan_section_ms[k] = (double)ticks[k] / (double)c->wall_khz;
   return TSW_OK;
 }

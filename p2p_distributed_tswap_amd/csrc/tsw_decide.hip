@@ -74,9 +74,11 @@ __global__ void k_decide(DecideArgs A) {
     if (code == NH_UNKNOWN) {
       // queue the pair (two lanes racing on it may both queue it: K3 then resolves a
       // duplicate to the same code, which is harmless)
-      *p = NH_PENDING;
+      // reserve the queue slot first: a pair is marked PENDING only when it is really queued
+      // (past the capacity the host sees qcount > qcap and fails the call)
       const uint32_t qi = atomicAdd(A.qcount, 1u);
       if (qi < A.qcap) {
+        *p = NH_PENDING;
         AstarQuery q;
         q.v = v;
         q.goal = g;

@@ -1116,7 +1116,7 @@ uint32_t astar_wave_slots(const DevGrid& G, int num_cu, bool global_gs) {
 hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
                              uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
                              AstarQuery* ovf, uint32_t* novf, uint32_t hcap, bool global_gs, hipStream_t s,
-                             uint32_t* qnext) {
+                             uint32_t* qnext, uint32_t diag) {
   if (nq == 0) return hipSuccess;
   const uint32_t gs_lds = global_gs ? 0u : wave_gs_mode(G);
   hcap = hcap ? std::max<uint32_t>(4u, std::min(hcap, WAVE_HCAP)) : WAVE_HCAP;
@@ -1126,9 +1126,9 @@ hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq,
   const uint32_t grid = std::min(nq, nslots);
   hipError_t e = hipFuncSetAttribute((const void*)k_astar_wave, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  const uint32_t serial = getenv("TSW_ASTAR_SERIAL") ? 1u : 0u;  // A/B and tests: lone-lane core
+  const uint32_t serial = (diag & ASTAR_DIAG_SERIAL) ? 1u : 0u;  // A/B and tests: lone-lane core
   unsigned long long* prof = nullptr;
-  if (getenv("TSW_ASTAR_PROF")) {
+  if (diag & ASTAR_DIAG_PROF) {
     e = hipMalloc(&prof, (size_t)nq * 64u);
     if (e != hipSuccess) return e;
     hipMemsetAsync(prof, 0, (size_t)nq * 64u, s);
@@ -1153,6 +1153,33 @@ hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq,
             w[2] / 100.0 / np, (double)w[1] / std::max(1.0, w[2] / 100.0));
   }
   return e;
+}
+
+// Error recovery: every NH_PENDING code of the store back to NH_UNKNOWN (a K3 pass that failed
+// after its pairs were marked must not leave them pending for later calls). 8 codes per thread.
+__global__ void k_reset_pending(uint64_t* __restrict__ nh8, uint64_t n8) {
+  constexpr uint64_t ONES = 0x0101010101010101ull, HIGH = 0x8080808080808080ull;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t w = nh8[i];
+    // bytes equal to 0xFE: x = w ^ 0xFE.. has a zero byte there (classic zero-byte test, exact
+    // after masking out borrows with ~x)
+    const uint64_t x = w ^ (ONES * (uint64_t)NH_PENDING);
+    const uint64_t z = (x - ONES) & ~x & HIGH;
+    if (z) {
+      uint64_t out = w;
+      for (int b = 0; b < 8; ++b)
+        if (((w >> (8 * b)) & 0xFFu) == NH_PENDING) out |= 0xFFull << (8 * b);
+      nh8[i] = out;
+    }
+  }
+}
+
+hipError_t launch_reset_pending(uint8_t* nh, uint64_t nbytes, hipStream_t s) {
+  const uint64_t n8 = nbytes / 8u;  // table strides are multiples of 8
+  if (n8 == 0) return hipSuccess;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n8 + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_reset_pending, dim3(grid), dim3(256), 0, s, reinterpret_cast<uint64_t*>(nh), n8);
+  return hipGetLastError();
 }
 
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,

@@ -63,6 +63,30 @@ struct BlkBfsArgs {
 uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds);
 hipError_t launch_bfs_blk(const BlkBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
 
+// K1 v4 (tsw_bfs_big.hip): one WORKGROUP per goal over 8x8 cell blocks, free blocks and run
+// numbering read from global memory (L2-resident), for grids too large for k_bfs_blk's per-wave LDS.
+struct BigBfsArgs {
+  uint32_t W, H, BW, BH, Bp, nbp, cap, klog, bp_magic;
+  const uint64_t* frb;    // [nbp] padded free-cell blocks (global)
+  const uint32_t* abase;  // [nbp] first run-start index of block p (global)
+  const uint32_t* goals;
+  const uint32_t* slots;  // table slot per goal (nullptr: slot = goal index)
+  uint32_t k;
+  uint16_t* dist;
+  uint64_t dstride;
+  uint32_t nrs;
+  uint16_t* anch;         // per-workgroup compact anchor scratch, nrs u16 each
+  uint16_t* lovf;         // per-workgroup list overflow, 2 * nbp u16 each
+  uint64_t* wlg;          // per-workgroup west-step blocks, nbp u64 each
+  uint32_t* work;         // goal dequeue counter (zeroed before the launch)
+  uint32_t* err;
+  uint32_t vec16;
+  uint32_t scratch_wgs;   // workgroups the scratch buffers are sized for
+};
+bool bfs_big_fits(uint32_t nbp, int max_lds, uint32_t* cap_out);
+uint32_t bfs_big_workgroups(uint32_t nbp, uint32_t cap, int num_cu);
+hipError_t launch_bfs_big(const BigBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
+
 hipError_t launch_classify(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                            const uint16_t* dist_base, uint64_t stride, uint8_t* nh_base, hipStream_t s);
 
@@ -83,10 +107,16 @@ hipError_t launch_astar_lds(const DevGrid& G, const AstarQuery* Q, uint32_t nq, 
 // for queries whose byte-encoded g_scores overflowed).
 uint32_t astar_wave_slots(const DevGrid& G, int num_cu, bool global_gs = false);
 bool astar_wave_lds_gs(const DevGrid& G);  // k_astar_wave keeps this grid's g_scores in LDS
+// diagnostics of k_astar_wave (read once per context from the environment, tsw_capi.hip Tunables)
+constexpr uint32_t ASTAR_DIAG_SERIAL = 1u;  // lone-lane heap core instead of the wave-cooperative one
+constexpr uint32_t ASTAR_DIAG_PROF = 2u;    // per-query pop / clock profile printed to stderr
 hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq, uint8_t* nh_base, uint64_t nstride,
                              uint8_t* res, int32_t* lens, uint32_t* gs_all, uint32_t* epochs, uint32_t nslots,
                              AstarQuery* ovf, uint32_t* novf, uint32_t hcap /*0: default*/, bool global_gs,
-                             hipStream_t s, uint32_t* qnext = nullptr);
+                             hipStream_t s, uint32_t* qnext = nullptr, uint32_t diag = 0);
+
+// NH_PENDING -> NH_UNKNOWN over nbytes of next-hop codes (error recovery)
+hipError_t launch_reset_pending(uint8_t* nh, uint64_t nbytes, hipStream_t s);
 
 // Batched decentralized decision (tsw_decide.hip, agent.rs:329-462).
 constexpr uint32_t DEC_ACT_MOVE = 0, DEC_ACT_GOAL_SWAP = 1, DEC_ACT_ROTATION = 2, DEC_ACT_WAIT = 3;

@@ -167,22 +167,42 @@ __device__ void rules_init(const PlanArgs& P, const Arrays& S) {
   __syncthreads();
 }
 
-// Mark the (cell, goal) pair of agent k for K3 if it is not resolved; returns 1 if enqueued.
-__device__ __forceinline__ uint32_t enqueue_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab,
-                                                 uint32_t* s_q) {
+__device__ __forceinline__ void put_query(const PlanArgs& P, uint8_t* p, uint32_t qi, uint32_t v, uint32_t g,
+                                          int32_t tab) {
+  *p = NH_PENDING;  // only once the slot is ours: a pending code is always really queued
+  AstarQuery q;
+  q.v = v;
+  q.goal = g;
+  q.tab = tab;
+  q.out = qi;
+  P.Q[qi] = q;
+}
+
+// A pair a step needs now (the planner exits for K3 right after): queue it if it is unresolved.
+// Needed pairs are at most 2n per exit and the speculative ones stay below qcap/2, so the queue
+// (qcap = 4n + 4096) cannot overflow; if it ever did, the pair is not marked and the host, seeing
+// qcount > qcap, fails the call.
+__device__ __forceinline__ void enqueue_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q) {
   uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
-  if (*p != NH_UNKNOWN) return 0;  // PENDING: whoever flipped it enqueued it in this pass
-  *p = NH_PENDING;
+  if (*p != NH_UNKNOWN) return;  // PENDING: whoever flipped it enqueued it in this pass
   const uint32_t qi = atomicAdd(s_q, 1u);
-  if (qi < P.qcap) {
-    AstarQuery q;
-    q.v = v;
-    q.goal = g;
-    q.tab = tab;
-    q.out = qi;
-    P.Q[qi] = q;
+  if (qi < P.qcap) put_query(P, p, qi, v, g, tab);
+}
+
+// A speculative prefetch: the slot is reserved by CAS only while the queue holds fewer than
+// qcap/2 pairs, so prefetches never take the room the needed pairs of an exit rely on.
+__device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q) {
+  uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
+  if (*p != NH_UNKNOWN) return;
+  const uint32_t lim = P.qcap / 2u;
+  uint32_t cur = *(volatile uint32_t*)s_q;
+  for (;;) {
+    if (cur >= lim) return;
+    const uint32_t prev = atomicCAS(s_q, cur, cur + 1u);
+    if (prev == cur) break;
+    cur = prev;
   }
-  return 1;
+  put_query(P, p, cur, v, g, tab);
 }
 
 // parallel: refresh next-hop codes of agents whose code is dirty; unresolved pairs are
@@ -234,13 +254,13 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
     const uint8_t c = S.NHC[k];
     if (c < NH_STAY && S.V[k] != S.G[k]) {
       const uint32_t u = step_cell(S.V[k], c, P.W);
-      if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) enqueue_pair(P, u, S.G[k], tab, s_q);
+      if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) prefetch_pair(P, u, S.G[k], tab, s_q);
     }
     const uint32_t s = S.SUCC[k];
     if (s == SUCC_TERM || s == k) continue;
     if (!P.wide_prefetch && !(S.ONC[k] || S.V[s] == S.G[s])) continue;
     const uint32_t vs = S.V[s];
-    if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) enqueue_pair(P, vs, S.G[k], tab, s_q);
+    if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) prefetch_pair(P, vs, S.G[k], tab, s_q);
   }
   __syncthreads();
 }
@@ -259,12 +279,12 @@ __device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t
     const uint8_t c = S.NHC[k];
     if (c < NH_STAY && S.V[k] != S.G[k]) {
       const uint32_t u = step_cell(S.V[k], c, P.W);
-      if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) enqueue_pair(P, u, S.G[k], tab, s_q);
+      if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) prefetch_pair(P, u, S.G[k], tab, s_q);
     }
     const uint32_t s = S.SUCC[k];
     if (s == SUCC_TERM || s == k) continue;
     const uint32_t vs = S.V[s];
-    if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) enqueue_pair(P, vs, S.G[k], tab, s_q);
+    if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) prefetch_pair(P, vs, S.G[k], tab, s_q);
   }
   __syncthreads();
 }
@@ -283,7 +303,7 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
       if (tk >= 0 && (uint32_t)tk < P.m) {
         const uint32_t pc = P.pick[tk], dc = P.dlv[tk];
         const int32_t dt = P.goal_tab[dc];
-        if (dt >= 0 && pc != dc && P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) enqueue_pair(P, pc, dc, dt, s_q);
+        if (dt >= 0 && pc != dc && P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) prefetch_pair(P, pc, dc, dt, s_q);
       }
     }
     const int32_t tab = S.GT[k];
@@ -294,7 +314,7 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
     for (uint32_t h = 0; h < hops && u != S.G[k]; ++h) {
       const uint8_t cu = P.nh[(uint64_t)tab * P.nstride + u];
       if (cu == NH_UNKNOWN) {
-        enqueue_pair(P, u, S.G[k], tab, s_q);
+        prefetch_pair(P, u, S.G[k], tab, s_q);
         break;
       }
       if (cu >= NH_STAY) break;  // pending, or a stay code

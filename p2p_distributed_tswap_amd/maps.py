@@ -111,9 +111,22 @@ def sortation_map(w: int = 1024, h: int = 1024) -> list:
 
 
 def largest_component(rows) -> list:
-    """Cells (x, y) of the largest 4-connected free component, row-major order."""
+    """Cells (x, y) of the largest 4-connected free component, row-major order (ties: the
+    component met first in row-major order)."""
     blocked = rows_to_blocked(rows)
     h, w = blocked.shape
+    try:
+        from scipy import ndimage
+    except ImportError:  # pragma: no cover - scipy is in the image; the loop below is the fallback
+        ndimage = None
+    if ndimage is not None:
+        lab, nlab = ndimage.label(~blocked)  # default structure = 4-connectivity in 2-D
+        if nlab == 0:
+            return []
+        sizes = np.bincount(lab.reshape(-1))[1:]
+        best_id = int(np.argmax(sizes)) + 1  # labels are numbered in raster order of first cell
+        ys, xs = np.nonzero(lab == best_id)
+        return [(int(x), int(y)) for y, x in zip(ys, xs)]
     comp = -np.ones((h, w), dtype=np.int64)
     best, best_id, cid = 0, -1, 0
     for sy in range(h):
@@ -224,9 +237,55 @@ def read_movingai(path: str, passable: str = ".GS") -> list:
     return ["".join(c if c in passable else "@" for c in r).replace("G", ".").replace("S", ".") for r in rows]
 
 
+def make_window_instance(rows, n_agents: int, n_tasks: int, seed: int, x0: int, y0: int, w: int, h: int):
+    """As make_instance, but starts and task cells are drawn from the window [x0, x0+w) x [y0, y0+h)
+    of the largest component: dense traffic (C5 — "dense rotation cycles") on a large floor."""
+    cells = [c for c in largest_component(rows) if x0 <= c[0] < x0 + w and y0 <= c[1] < y0 + h]
+    r = SplitMix64(seed ^ 0x5A5A5A5A)
+    pool = list(cells)
+    r.shuffle(pool)
+    if n_agents > len(pool):
+        raise ValueError("more agents than free cells in the window")
+    starts = np.array(pool[:n_agents], dtype=np.uint32).reshape(-1, 2)
+    tasks = np.zeros((n_tasks, 4), dtype=np.uint32)
+    nc = len(cells)
+    for k in range(n_tasks):
+        a = r.below(nc)
+        b = r.below(nc - 1)
+        if b >= a:
+            b += 1
+        tasks[k] = (*cells[a], *cells[b])
+    return starts, tasks
+
+
+def c5_instance(n_agents: int = 10000, n_tasks: int = 10000, seed: int = 0x1024):
+    """C5: the 1024x1024 sortation floor, agents and task cells packed into the central
+    160x160 window (~24k free cells, 10k agents = ~42% occupancy): dense traffic, rule-3 swaps and
+    rule-4 rotation cycles every step. Returns (rows, starts, tasks)."""
+    rows = sortation_map(1024, 1024)
+    starts, tasks = make_window_instance(rows, n_agents, n_tasks, seed, 432, 432, 160, 160)
+    return rows, starts, tasks
+
+
 CONFIGS = {
     # name: (map factory, n_agents, n_tasks, instance seed)  — BASELINE.json configs
     "c1_bundled_10": (bundled_map, 10, 30, 1),
     "c2_random_32_32_20": (lambda: random_map(32, 32, 0.20, 0x3232), 200, 600, 0x3232),
     "c3_warehouse_170x84": (lambda: warehouse_map(170, 84, 0x170084), 1000, 3000, 0x170084),
+    # K1-only config: 10,000 distinct goal cells (BFS tables), goal-sharded over 2/4/8 GPUs
+    "c4_den520d_10k_goals": (lambda: cave_map(256, 257, 0x520D), 0, 0, 0x520D),
+    # dense MAPD on the sortation floor: instance from c5_instance() (window-packed, not make_instance)
+    "c5_sortation_1024_10k": (lambda: sortation_map(1024, 1024), 10000, 10000, 0x1024),
 }
+# distinct K1 goals of the table-build configs
+CONFIG_GOALS = {"c4_den520d_10k_goals": 10000, "c5_sortation_1024_10k": 10000}
+
+
+def config_instance(name: str):
+    """(rows, starts, tasks) of a MAPD config of CONFIGS."""
+    if name == "c5_sortation_1024_10k":
+        return c5_instance()
+    fac, n, m, seed = CONFIGS[name]
+    rows = fac()
+    starts, tasks = make_instance(rows, n, m, seed)
+    return rows, starts, tasks

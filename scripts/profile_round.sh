@@ -1,16 +1,23 @@
 #!/bin/bash
 # Profiles the default bench on one MI355X (run through gpurun from the repo root).
-#   1. bench.py (HIP-event timings, CPU baseline)            -> $OUT/bench.json
-#   2. rocprofv3 --kernel-trace --stats of the same command   -> $OUT/trace/
-#   3. separate PMC passes: FETCH_SIZE, WRITE_SIZE            -> $OUT/pmc_fetch, $OUT/pmc_write
+#   1. bench.py, the driver's default command                      -> $OUT/bench.json
+#   2. per workload (plan = the C3 planning leg, bfs = K1 on den520d, 10k goals), each its own
+#      process so no kernel's launches mix workloads:
+#        rocprofv3 --kernel-trace --stats                           -> $OUT/<wl>_trace/
+#        separate PMC passes FETCH_SIZE and WRITE_SIZE              -> $OUT/<wl>_pmc_fetch, _pmc_write
+# Then: python scripts/summarize_profile.py $OUT profiles/<tag>
 # Each GPU step has its own time limit; steps are chained with && so a failure stops the run.
 set -o pipefail
-TAG=${1:-r1}
+TAG=${1:-r2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS="--steps 1 --warmup 0 --no-cpu --bfs-reps 1"
-timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 > $OUT/bench.json 2> $OUT/bench.err &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 &&
-timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py $ARGS > $OUT/pmc_fetch.log 2>&1 &&
-timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py $ARGS > $OUT/pmc_write.log 2>&1
+PLAN="--steps 1 --warmup 0 --no-cpu --no-bfs"
+BFS="--no-plan --no-cpu --bfs-reps 2"
+timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err &&
+for WL in plan bfs; do
+  if [ $WL = plan ]; then A=$PLAN; else A=$BFS; fi
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${WL}_trace -o run -- python3 bench.py $A > $OUT/${WL}_trace.json 2> $OUT/${WL}_trace.err &&
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/${WL}_pmc_fetch -o run -- python3 bench.py $A > $OUT/${WL}_pmc_fetch.json 2> $OUT/${WL}_pmc_fetch.err &&
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/${WL}_pmc_write -o run -- python3 bench.py $A > $OUT/${WL}_pmc_write.json 2> $OUT/${WL}_pmc_write.err || exit 1
+done

@@ -9,7 +9,8 @@ with the GPU's. CPU whole-plan time is extrapolated from the prefix rate (labell
 
 usage: python scripts/scale_bench.py [instance ...] [--cpu-steps N]
 instances: c3 (warehouse 170x84, 1,000 agents, 3,000 tasks — BASELINE configs[2]),
-           wh10k (warehouse 510x220, 10,000 agents, 30,000 tasks)
+           wh10k (warehouse 510x220, 10,000 agents, 30,000 tasks — the north_star instance),
+           c5 (1024x1024 sortation floor, 10,000 agents packed in a 160x160 window — configs[4])
 """
 import argparse
 import json
@@ -23,10 +24,16 @@ import numpy as np  # noqa: E402
 
 from p2p_distributed_tswap_amd import Planner, maps  # noqa: E402
 
-# name: (map factory, agents, tasks, seed, CPU prefix timesteps)
+def _wh10k():
+    rows = maps.warehouse_map(510, 220, 0x510220)
+    return (rows, *maps.make_instance(rows, 10000, 30000, 0x510220))
+
+
+# name: (instance factory -> (rows, starts, tasks), CPU prefix timesteps)
 INSTANCES = {
-    "c3": (lambda: maps.warehouse_map(170, 84, 0x170084), 1000, 3000, 0x170084, 20),
-    "wh10k": (lambda: maps.warehouse_map(510, 220, 0x510220), 10000, 30000, 0x510220, 3),
+    "c3": (lambda: maps.config_instance("c3_warehouse_170x84"), 20),
+    "wh10k": (_wh10k, 3),
+    "c5": (maps.c5_instance, 2),
 }
 
 
@@ -48,11 +55,11 @@ def main():
     from oracle import OracleGraph  # CPU baseline + prefix check only
 
     for name in args.instances:
-        fac, n, m, seed, cpu_steps = INSTANCES[name]
+        fac, cpu_steps = INSTANCES[name]
         cpu_steps = args.cpu_steps or cpu_steps
-        rows = fac()
+        rows, starts, tasks = fac()
+        n, m = starts.shape[0], tasks.shape[0]
         h, w = len(rows), len(rows[0])
-        starts, tasks = maps.make_instance(rows, n, m, seed)
         with Planner(rows) as p:
             p.plan_mapd_arrays(starts[:8], tasks[:8], 4)  # context warm-up (not timed)
             p.clear_tables()

@@ -1,13 +1,22 @@
 """Summarise a scripts/profile_round.sh output directory into profiles/<tag>/.
 
-Copies the rocprofv3 --kernel-trace --stats summary and writes summary.json with, per kernel:
-average duration (kernel trace), calls, and per-launch HBM traffic from the separate PMC passes.
+Per workload (plan = the bench's planning leg, bfs = K1 alone on den520d, 10,000 goals; each
+profiled in its own process so launches of different sizes never mix):
+  * copies the rocprofv3 --kernel-trace --stats summary  -> profiles/<tag>/<wl>_kernel_stats.csv
+  * per kernel CLASS (K1 = k_bfs*/k_classify, K3 = k_astar*/k_enqueue_unknown, k_plan):
+      device ns per launch from the kernel trace, HBM bytes per launch from the separate PMC
+      passes, and the algorithmic bytes per launch the bench reports for that class.
+Launch = what bench.py counts for the class (HIP-event brackets: one K3 pass may dispatch up to
+three A* kernels; K1 in the bfs workload = one k_bfs_blk dispatch).
 Traffic correction (/opt/skills/guides/MI355X_MICROARCH.md, "HBM"): FETCH_SIZE and WRITE_SIZE are
 in KB; on gfx950 FETCH_SIZE reports half the bytes of wide coalesced streaming reads, so
 read bytes = 2 * FETCH_SIZE * 1024 (an upper bound for narrow/scattered reads, which the guide
 lists as uncalibrated); write bytes = WRITE_SIZE * 1024.
 
-Usage: python scripts/summarize_profile.py gpurun_out/prof_r1 profiles/r1
+Writes profiles/<tag>/pmc.json, read by bench.py (profiled_traffic) only when the workload and
+its algorithmic bytes per launch match the live run.
+
+Usage: python scripts/summarize_profile.py gpurun_out/prof_r2 profiles/r2
 """
 from __future__ import annotations
 
@@ -18,43 +27,92 @@ import os
 import shutil
 import sys
 
+WORKLOADS = {"plan": "plan:c3_warehouse_170x84", "bfs": "bfs:den520d_10k"}
+
 
 def short(name: str) -> str:
     base = name.split("(")[0]
-    return base.replace("void ", "").replace("tsw::", "")
+    return base.replace("void ", "").replace("tsw::", "").split("<")[0]
+
+
+def kclass(name: str):
+    k = short(name)
+    if k.startswith("k_astar") or k.startswith("k_enqueue_unknown"):
+        return "K3"
+    if k.startswith("k_plan"):
+        return "k_plan"
+    if k.startswith("k_bfs") or k.startswith("k_classify"):
+        return "K1"
+    return None
+
+
+def bench_line(path: str):
+    try:
+        for ln in open(path):
+            if ln.startswith('{"metric"'):
+                return json.loads(ln)
+    except OSError:
+        pass
+    return None
 
 
 def main(src: str, dst: str):
     os.makedirs(dst, exist_ok=True)
-    out = {"source": src, "kernels": {}}
-    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
-    if os.path.exists(stats):
-        shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
-        for r in csv.DictReader(open(stats)):
-            k = short(r["Name"])
-            out["kernels"].setdefault(k, {})
-            out["kernels"][k].update(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
-                                     total_ns=float(r["TotalDurationNs"]), pct=float(r["Percentage"]))
-    for tag, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
-        p = os.path.join(src, tag, "run_counter_collection.csv")
-        if not os.path.exists(p):
+    out = {"source": src, "correction": "read = 2*FETCH_SIZE KB, write = WRITE_SIZE KB (gfx950)", "workloads": {}}
+    for wl, key in WORKLOADS.items():
+        stats = os.path.join(src, f"{wl}_trace", "run_kernel_stats.csv")
+        line = bench_line(os.path.join(src, f"{wl}_trace.json"))
+        if not os.path.exists(stats) or line is None:
             continue
-        agg = collections.defaultdict(list)
-        for r in csv.DictReader(open(p)):
-            if r["Counter_Name"] == counter:
-                agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-        for k, v in agg.items():
-            d = out["kernels"].setdefault(k, {})
-            d[counter + "_KB_per_launch"] = sum(v) / len(v)
-    for k, d in out["kernels"].items():
-        if "FETCH_SIZE_KB_per_launch" in d and "WRITE_SIZE_KB_per_launch" in d:
-            d["hbm_bytes_per_launch"] = 2 * d["FETCH_SIZE_KB_per_launch"] * 1024 + d["WRITE_SIZE_KB_per_launch"] * 1024
+        shutil.copy(stats, os.path.join(dst, f"{wl}_kernel_stats.csv"))
+        cls = collections.defaultdict(lambda: {"device_ns": 0.0, "dispatches": 0, "kernels": {}})
+        for r in csv.DictReader(open(stats)):
+            c = kclass(r["Name"])
+            if c is None:
+                continue
+            cls[c]["device_ns"] += float(r["TotalDurationNs"])
+            cls[c]["dispatches"] += int(r["Calls"])
+            cls[c]["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+        # launches and algorithmic bytes per launch as the bench counts them
+        if wl == "plan":
+            ref = (line.get("roofline") or {}).get("classes", {})
+            launches = {c: d["launches"] for c, d in ref.items()}
+            algo = {c: d["algorithmic_bytes_per_launch"] for c, d in ref.items()}
+        else:
+            b = line["bfs"]["roofline"]
+            launches = {"K1": cls["K1"]["kernels"].get("k_bfs_blk", {}).get("calls", cls["K1"]["dispatches"])}
+            algo = {"K1": b["algorithmic_bytes_per_launch"]}
+        for tag, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+            p = os.path.join(src, f"{wl}_{tag}", "run_counter_collection.csv")
+            if not os.path.exists(p):
+                continue
+            tot = collections.defaultdict(float)
+            for r in csv.DictReader(open(p)):
+                if r["Counter_Name"] == counter:
+                    c = kclass(r["Kernel_Name"])
+                    if c:
+                        tot[c] += float(r["Counter_Value"])
+            for c, v in tot.items():
+                cls[c][counter + "_KB_total"] = v
+        res = {}
+        for c, d in cls.items():
+            L = max(int(launches.get(c, 0)), 1)
+            e = {"launches": L, "dispatches": d["dispatches"], "device_us_per_launch": d["device_ns"] / L / 1e3,
+                 "kernels": d["kernels"], "algorithmic_bytes_per_launch": algo.get(c)}
+            if "FETCH_SIZE_KB_total" in d and "WRITE_SIZE_KB_total" in d:
+                e["read_bytes_per_launch"] = 2 * d["FETCH_SIZE_KB_total"] * 1024 / L
+                e["write_bytes_per_launch"] = d["WRITE_SIZE_KB_total"] * 1024 / L
+                e["hbm_bytes_per_launch"] = e["read_bytes_per_launch"] + e["write_bytes_per_launch"]
+                if algo.get(c):
+                    e["traffic_over_algorithmic"] = e["hbm_bytes_per_launch"] / algo[c]
+            res[c] = e
+        out["workloads"][key] = res
     bj = os.path.join(src, "bench.json")
     if os.path.exists(bj):
         shutil.copy(bj, os.path.join(dst, "bench.json"))
-    with open(os.path.join(dst, "summary.json"), "w") as f:
+    with open(os.path.join(dst, "pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps(out, indent=1)[:3000])
+    print(json.dumps(out, indent=1)[:4000])
 
 
 if __name__ == "__main__":

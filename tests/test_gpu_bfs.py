@@ -1,5 +1,6 @@
-"""K1 parity: the three BFS kernels (k_bfs_blk: one wavefront per goal over 8x8 blocks;
-k_bfs_wave: one wavefront per goal over row words; k_bfs: one workgroup per goal) against the oracle's BFS (oracle/tswap_oracle.c, cross-checked against A* path lengths in
+"""K1 parity: the four BFS kernels (k_bfs_blk: one wavefront per goal over 8x8 blocks;
+k_bfs_wave: one wavefront per goal over row words; k_bfs: one workgroup per goal over row words;
+k_bfs_big: one workgroup per goal over 8x8 blocks, the large-grid kernel) against the oracle's BFS (oracle/tswap_oracle.c, cross-checked against A* path lengths in
 test_oracle.py), bit-exact, on ragged widths, list-overflow paths and the full-size den520d-like
 cave (BASELINE configs[3])."""
 import os
@@ -65,7 +66,7 @@ def _goals(rows, n, seed):
     return rng.choice(free, size=min(n, free.size), replace=False).astype(np.uint32)
 
 
-@pytest.mark.parametrize("kernel", ["blk", "wave", "block"])
+@pytest.mark.parametrize("kernel", ["blk", "wave", "block", "big"])
 @pytest.mark.parametrize("name", sorted(GRIDS))
 def test_bfs_kernels_bit_exact(kernel, name):
     rows = GRIDS[name]()
@@ -85,7 +86,7 @@ def test_bfs_blk_list_overflow(cap):
     _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="blk", TSW_BFS_BLKCAP=cap)
 
 
-@pytest.mark.parametrize("kernel", ["blk", "wave"])
+@pytest.mark.parametrize("kernel", ["blk", "wave", "big"])
 def test_bfs_wave_unreachable_pockets(kernel):
     """Walled-off pockets stay 0xFFFF; goals inside a pocket see only the pocket."""
     a = np.zeros((40, 70), dtype=bool)
@@ -122,7 +123,7 @@ class _DevBuf:
         self.hip.hipFree(self.ptr)
 
 
-@pytest.mark.parametrize("kernel", ["blk", "wave"])
+@pytest.mark.parametrize("kernel", ["blk", "wave", "big"])
 def test_bfs_den520d_full_size(kernel):
     """BASELINE configs[3] geometry: 256x257 cave, 1,000 distinct goals through the device-output
     entry point the bench times (16-B stores), every table bit-exact vs the oracle."""
@@ -140,7 +141,7 @@ def test_bfs_den520d_full_size(kernel):
         assert np.array_equal(got[k], ref), f"goal {g}: {np.count_nonzero(got[k] != ref)} cells differ"
 
 
-@pytest.mark.parametrize("kernel", ["blk", "wave"])
+@pytest.mark.parametrize("kernel", ["blk", "wave", "big"])
 def test_bfs_symmetry_full_goal_set(kernel):
     """Size-independent property at full size: d_g(c) == d_c(g) for every pair of goals, over all
     free cells of a 96x97 cave used as goals (the table matrix restricted to goals is symmetric),

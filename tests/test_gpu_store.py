@@ -1,0 +1,91 @@
+"""GPU: the goal-table store — LRU eviction under a small table_budget_bytes, ENOMEM only when one
+call's goals do not fit, and a failed K1 build (u16 distance overflow) that leaves the context
+clean (no goal registered against a partial table). Results bit-exact vs the oracle throughout.
+
+Reference semantics: the per-tick step (tswap.rs:174-286, manager.rs:147-259) on a goal stream
+whose cells change every tick (task injection, manager.rs:367-436; rule 3, tswap.rs:198-202)."""
+import numpy as np
+import pytest
+
+from p2p_distributed_tswap_amd import TSW_ENOMEM, TSW_EOVERFLOW, Planner, TswapError, maps
+from oracle import OracleGraph
+
+pytestmark = pytest.mark.gpu
+
+
+def _cells(rows):
+    cells = maps.rows_to_array(rows)
+    comp = maps.largest_component(rows)
+    return cells, np.array([y * cells.shape[1] + x for (x, y) in comp], dtype=np.uint32)
+
+
+def test_step_streams_goals_through_small_budget():
+    """30 ticks, 20 agents, fresh random goals every tick (~600 distinct goals) through a store of
+    64 tables: tables are evicted least-recently-used and rebuilt on demand, every tick exact."""
+    rows = maps.random_map(32, 32, 0.20, 0x3232)
+    cells, cid = _cells(rows)
+    og = OracleGraph(cells)
+    per_table = ((32 * 32 + 7) // 8 * 8) * 3
+    rng = np.random.default_rng(21)
+    n = 20
+    v = cid[rng.choice(cid.size, n, replace=False)]
+    with Planner(rows, table_budget_bytes=64 * per_table) as p:
+        for tick in range(30):
+            g = cid[rng.choice(cid.size, n, replace=True)]
+            g[: n // 4] = v[: n // 4]
+            rv, rg = og.step(v, g)
+            hv, hg = p.step(v, g)
+            assert np.array_equal(hv, rv) and np.array_equal(hg, rg), f"tick {tick}"
+            v = rv
+        st = p.stats()
+    assert st["table_evictions"] > 0
+    assert st["tables"] <= 64
+
+
+def test_budget_too_small_for_one_call_then_recovers():
+    rows = maps.random_map(32, 32, 0.20, 0x3232)
+    cells, cid = _cells(rows)
+    og = OracleGraph(cells)
+    per_table = ((32 * 32 + 7) // 8 * 8) * 3
+    goals = cid[:40]
+    with Planner(rows, table_budget_bytes=16 * per_table) as p:
+        with pytest.raises(TswapError) as ei:
+            p.dist_tables(goals)
+        assert ei.value.code == TSW_ENOMEM
+        got = p.dist_tables(goals[:10])  # the failed call left nothing half-registered
+        for k, g in enumerate(goals[:10]):
+            assert np.array_equal(got[k], og.bfs(int(g)))
+        v = goals[:8].copy()
+        g = goals[8:16].copy()
+        rv, rg = og.step(v, g)
+        hv, hg = p.step(v, g)
+        assert np.array_equal(hv, rv) and np.array_equal(hg, rg)
+
+
+def _serpentine_plus_room():
+    """512x512: a serpentine (every other row a wall with one gap, alternating ends: >131k steps
+    end to end, past the u16 table range) above a wall, an open 512x64 room below it."""
+    a = np.zeros((512, 512), dtype=bool)
+    for i, y in enumerate(range(1, 440, 2)):
+        a[y, :] = True
+        a[y, 511 if i % 2 else 0] = False
+    a[441, :] = True  # closes the serpentine off from the room
+    return maps.to_rows(a)
+
+
+def test_k1_distance_overflow_leaves_context_clean():
+    rows = _serpentine_plus_room()
+    cells = maps.rows_to_array(rows)
+    far = np.array([0], dtype=np.uint32)                       # serpentine entry: eccentricity > 65534
+    room = np.array([480 * 512 + 7, 500 * 512 + 300], dtype=np.uint32)
+    og = OracleGraph(cells)
+    with Planner(rows) as p:
+        for _ in range(2):  # fails again: the first failure did not register a partial table
+            with pytest.raises(TswapError) as ei:
+                p.dist_tables(far)
+            assert ei.value.code == TSW_EOVERFLOW
+        assert p.stats()["tables"] == 0
+        got = p.dist_tables(room)
+        for k, g in enumerate(room):
+            assert np.array_equal(got[k], og.bfs(int(g)))
+        assert p.stats()["tables"] == 2
