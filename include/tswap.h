@@ -194,6 +194,10 @@ typedef struct {
      * (same indices as plan_section_ms; [7] = relaunch entry) */
     uint64_t plan_exits[8];
     uint64_t table_evictions;   /* goal tables dropped by the LRU (table_budget_bytes reached) */
+    /* coop mode (K3 workers running concurrently with the planner): times the planner waited for
+     * a worker, and its total waiting time (inside walker_ms) */
+    uint64_t coop_waits;
+    double coop_wait_ms;
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

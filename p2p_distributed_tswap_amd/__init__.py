@@ -88,6 +88,7 @@ class Stats(ctypes.Structure):
         ("steps", ctypes.c_uint64), ("tables", ctypes.c_uint64), ("plan_ms", ctypes.c_double),
         ("plan_section_ms", ctypes.c_double * 8), ("rule_rounds", ctypes.c_uint64),
         ("plan_exits", ctypes.c_uint64 * 8), ("table_evictions", ctypes.c_uint64),
+        ("coop_waits", ctypes.c_uint64), ("coop_wait_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

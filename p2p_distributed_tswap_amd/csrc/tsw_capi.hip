@@ -63,6 +63,7 @@ struct Tunables {
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
   uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
+  bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
 
   static Tunables from_env() {
     Tunables t;
@@ -88,6 +89,7 @@ struct Tunables {
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
     t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
+    t.coop = num("TSW_COOP", 0, 1, 1) != 0;
     return t;
   }
 };
@@ -155,6 +157,15 @@ struct tsw_ctx {
   uint8_t* d_res = nullptr;
   int32_t* d_lens = nullptr;
   size_t rescap = 0;
+
+  // coop mode: K3 workers concurrent with the planner (second stream, control block, queues)
+  hipStream_t s2 = nullptr;
+  CoopCtl* d_cc = nullptr;
+  CoopCtl* h_cc = nullptr;       // pinned
+  AstarQuery* d_QS = nullptr;
+  size_t qscap = 0;
+  uint32_t* h_started = nullptr; // pinned, coherent: set by the planner block when resident
+  uint32_t* d_started = nullptr;
 
   DevStatus* d_stat = nullptr;
   DevStatus* h_stat = nullptr;   // pinned, D2H
@@ -886,6 +897,25 @@ int ensure_agents(tsw_ctx* c, size_t n) {
   return TSW_OK;
 }
 
+// Coop-mode buffers: control block, speculative queue, the needed queue sized for a whole launch,
+// the second stream and the host-visible "planner resident" flag.
+int ensure_coop(tsw_ctx* c, uint32_t n) {
+  TRY(ensure_astar_scratch(c));
+  TRY(ensure_queue(c, std::max<size_t>(4 * (size_t)n + 4096, (size_t)1 << 18)));
+  if (!c->d_cc) {
+    HIPCHK(hipMalloc(&c->d_cc, sizeof(CoopCtl)));
+    HIPCHK(hipHostMalloc(&c->h_cc, sizeof(CoopCtl), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&c->h_started, 4, hipHostMallocCoherent | hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void**)&c->d_started, c->h_started, 0));
+    HIPCHK(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
+  }
+  if (!c->d_QS) {
+    HIPCHK(hipStreamSynchronize(c->s));
+    HIPCHK(dgrow(c->d_QS, c->qscap, (size_t)1 << 20));
+  }
+  return TSW_OK;
+}
+
 PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_goals) {
   PlanArgs P{};
   P.n = n;
@@ -943,6 +973,14 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.agents_lds = ag;
   P.occ_lds = oc;
   P.tasks_lds = tk;
+  // coop mode: lazy next hops only (eager tables have nothing left to resolve)
+  P.coop = (c->tun.coop && P.prefetch && c->d_cc && c->d_QS) ? 1u : 0u;
+  if (P.coop) {
+    P.QS = c->d_QS;
+    P.qscap = (uint32_t)c->qscap;
+    P.cc = c->d_cc;
+    P.started = c->d_started;
+  }
   return P;
 }
 
@@ -963,15 +1001,61 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   // one lane per agent in the parallel passes when possible; >= 4 waves for the task argmin
   uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
   if (c->tun.plan_block) block = std::max<uint32_t>(64u, c->tun.plan_block);
+  const bool coop = P.coop != 0;
+  WorkerArgs W{};
+  uint32_t waves = 0;
+  if (coop) {
+    W.G = c->G;
+    W.cc = c->d_cc;
+    W.QN = c->d_Q;
+    W.QS = c->d_QS;
+    W.nh = c->d_nh;
+    W.nstride = c->tstride;
+    W.hcap = c->tun.wave_hcap;
+    W.gs_all = c->d_gs;
+    W.epochs = c->d_epochs;
+    W.heaps = c->d_heaps;
+    W.ghcap = c->hcap;
+    waves = std::min(worker_waves(c->G, c->num_cu), c->nslots);
+  }
   for (uint64_t round = 0;; ++round) {
     if (round > 16ull * P.n + 4096ull * (init.max_t + 1)) RET(TSW_EINVAL, "plan kernel made no progress");
+    if (coop) {
+      HIPCHK(hipMemsetAsync(c->d_cc, 0, sizeof(CoopCtl), c->s));
+      *(volatile uint32_t*)c->h_started = 0u;
+    }
     {
       Timer t(c, CAT_WALK);
       HIPCHK(launch_plan(P, lds, block, c->s));
     }
     c->st.walker_launches++;
+    if (coop) {
+      // the workers go on the second stream once the planner block is resident (it sets the flag
+      // first thing), so they can never take the CU it needs; if the flag is late they start anyway
+      // and the planner falls back to exits (no deadlock either way)
+      const auto t0 = std::chrono::steady_clock::now();
+      while (!*(volatile uint32_t*)c->h_started &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500)) {
+      }
+      HIPCHK(launch_astar_workers(W, waves, c->s2));
+      c->st.astar_launches++;
+    }
     HIPCHK(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(PlanCtl), hipMemcpyDeviceToHost, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
+    if (coop) {
+      HIPCHK(hipStreamSynchronize(c->s2));
+      HIPCHK(hipMemcpy(c->h_cc, c->d_cc, sizeof(CoopCtl), hipMemcpyDeviceToHost));
+      const CoopCtl& cc = *c->h_cc;
+      c->st.coop_waits += cc.waits;
+      c->st.coop_wait_ms += (double)cc.wait_ticks / (double)c->wall_khz;
+      c->st.astar_queries += cc.worker_queries;
+      if (cc.err) RET(TSW_EOVERFLOW, "K3 worker: A* heap overflow");
+      // speculative pairs nobody claimed stay PENDING_S: back to UNKNOWN for later calls
+      if (cc.head_s > cc.claim_s) {
+        HIPCHK(launch_reset_pending(c->d_nh, (uint64_t)c->tab_count * c->tstride, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+      }
+    }
     const PlanCtl& k = *c->h_ctl;
     if (k.err) {
       char buf[128];
@@ -989,18 +1073,22 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                 (unsigned long long)round + 1ull, tk[8] / 100.0, tk[9] / 100.0, tk[10] / 100.0, tk[11] / 100.0,
                 tk[12] / 100.0, tk[13] / 100.0, tk[14] / 100.0, tk[15] / 100.0);
       }
-      // pairs the rules prefetch queued but no firing needed: resolve them so no table entry
-      // is left PENDING for later calls
-      if (k.qcount > 0) {
+      // exit mode: pairs the prefetch queued but no firing needed — resolve them so no table entry
+      // is left PENDING for later calls (coop mode: the workers drained the needed queue)
+      if (!coop && k.qcount > 0) {
         if (k.qcount > P.qcap) RET(TSW_EINVAL, "plan kernel queue overflow");
         TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
         TRY(check_err(c));
       }
       return TSW_OK;
     }
+    c->st.plan_exits[std::min<uint32_t>(k.section, 7u)]++;
+    if (coop) {
+      if (k.status != PLAN_NEED_QUERIES) RET(TSW_EINVAL, "plan kernel stopped without resolvable next hops");
+      continue;  // the workers resolved every needed pair before exiting: relaunch
+    }
     if (k.status != PLAN_NEED_QUERIES || k.qcount == 0 || k.qcount > P.qcap)
       RET(TSW_EINVAL, "plan kernel stopped without resolvable next hops");
-    c->st.plan_exits[std::min<uint32_t>(k.section, 7u)]++;
     TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
     TRY(check_err(c));
   }
@@ -1073,6 +1161,7 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   TRY(build_occ(c, n));
   TRY(ensure_tables(c, goalset));
   TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
+  if (c->tun.coop && !eager_policy(c, 0)) TRY(ensure_coop(c, n));
   PlanArgs P = plan_args(c, n, m, MODE_MAPD, goal_out != nullptr);
   PlanCtl init{};
   init.section = SEC_ASSIGN;
@@ -1261,6 +1350,10 @@ void tsw_destroy(tsw_ctx* c) {
   if (c->h_dups) (void)hipHostFree(c->h_dups);
   fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
+  fre(c->d_cc); fre(c->d_QS);
+  if (c->h_cc) (void)hipHostFree(c->h_cc);
+  if (c->h_started) (void)hipHostFree(c->h_started);
+  if (c->s2) (void)hipStreamDestroy(c->s2);
   if (c->h_stat) hipHostFree(c->h_stat);
   if (c->h_ctl) hipHostFree(c->h_ctl);
   for (auto& e : c->pending) {
@@ -1303,6 +1396,7 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   TRY(build_occ(c, n));
   TRY(ensure_tables(c, goals));
   TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
+  if (c->tun.coop && !eager_policy(c, 0)) TRY(ensure_coop(c, n));
   PlanArgs P = plan_args(c, n, 0, MODE_STEP, false);
   PlanCtl init{};
   init.section = SEC_PRE1;

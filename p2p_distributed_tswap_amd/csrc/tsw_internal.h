@@ -21,7 +21,8 @@
 namespace tsw {
 
 constexpr uint8_t NH_STAY = 4;
-constexpr uint8_t NH_PENDING = 0xFE;
+constexpr uint8_t NH_PENDING_S = 0xFD;  // queued speculatively for the concurrent K3 workers (coop mode)
+constexpr uint8_t NH_PENDING = 0xFE;    // queued for a K3 pass (needed)
 constexpr uint8_t NH_UNKNOWN = 0xFF;
 constexpr uint16_t DIST_INF = 0xFFFF;
 constexpr uint8_t NB_FREE = 0x80;
@@ -49,6 +50,20 @@ struct Tables {
   int32_t* goal_tab;
   uint32_t* tab_goal;
   uint64_t tstride;  // elements per table (dist and nh)
+};
+
+// Concurrent K3 (coop mode): the planner publishes queued pairs, persistent A* worker waves on the
+// other CUs claim and resolve them while the planner keeps running (tsw_plan.hip, k_astar_worker).
+// Counters live on separate 128-B lines (claimed by CAS from many CUs, polled by the planner).
+struct CoopCtl {
+  uint32_t head_n, pad0[31];   // needed queue: entries published by the planner
+  uint32_t claim_n, pad1[31];  // needed queue: entries claimed by workers
+  uint32_t head_s, pad2[31];   // speculative queue: published
+  uint32_t claim_s, pad3[31];  // speculative queue: claimed
+  uint32_t stop, alive, err, waits;  // planner finished / workers started / worker error bits / planner waits
+  unsigned long long wait_ticks;     // planner time spent waiting on workers (100 MHz ticks)
+  unsigned long long worker_queries; // queries resolved by workers
+  uint32_t pad4[24];
 };
 
 struct AstarQuery {

@@ -20,6 +20,7 @@
 
 #include "tsw_internal.h"
 #include "tsw_launch.h"
+#include "tsw_plan.h"
 
 namespace tsw {
 
@@ -1155,7 +1156,7 @@ hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq,
   return e;
 }
 
-// Error recovery: every NH_PENDING code of the store back to NH_UNKNOWN (a K3 pass that failed
+// Error recovery: every NH_PENDING / NH_PENDING_S code of the store back to NH_UNKNOWN (a K3 pass that failed
 // after its pairs were marked must not leave them pending for later calls). 8 codes per thread.
 __global__ void k_reset_pending(uint64_t* __restrict__ nh8, uint64_t n8) {
   constexpr uint64_t ONES = 0x0101010101010101ull, HIGH = 0x8080808080808080ull;
@@ -1163,12 +1164,16 @@ __global__ void k_reset_pending(uint64_t* __restrict__ nh8, uint64_t n8) {
     const uint64_t w = nh8[i];
     // bytes equal to 0xFE: x = w ^ 0xFE.. has a zero byte there (classic zero-byte test, exact
     // after masking out borrows with ~x)
-    const uint64_t x = w ^ (ONES * (uint64_t)NH_PENDING);
-    const uint64_t z = (x - ONES) & ~x & HIGH;
+    // bytes 0xFE / 0xFD: w ^ 0xFE.. / w ^ 0xFD.. has a zero byte there (classic zero-byte test,
+    // may flag a byte above a match too — the loop below checks each byte exactly)
+    const uint64_t x1 = w ^ (ONES * (uint64_t)NH_PENDING), x2 = w ^ (ONES * (uint64_t)NH_PENDING_S);
+    const uint64_t z = ((x1 - ONES) & ~x1 & HIGH) | ((x2 - ONES) & ~x2 & HIGH);
     if (z) {
       uint64_t out = w;
-      for (int b = 0; b < 8; ++b)
-        if (((w >> (8 * b)) & 0xFFu) == NH_PENDING) out |= 0xFFull << (8 * b);
+      for (int b = 0; b < 8; ++b) {
+        const uint32_t c = (uint32_t)((w >> (8 * b)) & 0xFFu);
+        if (c == NH_PENDING || c == NH_PENDING_S) out |= 0xFFull << (8 * b);
+      }
       nh8[i] = out;
     }
   }
@@ -1190,6 +1195,156 @@ hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const
   const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
   hipLaunchKernelGGL(k_enqueue_unknown, dim3(grid), dim3(256), 0, s, G, goals, slots, k, nh, nstride, Q, qcount,
                      qcap);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// Coop mode: persistent K3 worker waves running CONCURRENTLY with the planner (k_plan, one block).
+// The planner publishes queued (cell, goal) pairs in two queues of CoopCtl — needed pairs a step
+// is waiting on, and speculative prefetches — and keeps planning; each worker wave claims one pair
+// at a time (needed first, CAS on the claim counter), runs the same exact A* as k_astar_wave (same
+// BinaryHeap order, same hand-off chain: LDS heap + LDS g-scores -> LDS heap + global u32 g-scores
+// -> global heap), and stores the code into the next-hop table with an agent-scope store the
+// planner polls. Replaces the exit -> host sync -> K3 launch -> relaunch cycle of the exit mode:
+// speculative pairs resolve on the 255 otherwise idle CUs while the planner runs, and the planner
+// waits only for what a step needs.
+// Termination: when the planner sets `stop` the workers drain the needed queue and exit (unclaimed
+// speculative pairs are abandoned — the host resets them to UNKNOWN); an idle worker also exits
+// after 5 s without work, whatever the planner does.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t w_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool w_cas(uint32_t* p, uint32_t expect, uint32_t want) {
+  return __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// lane 0: claim the next pair (0: needed queue, 1: speculative queue, -1: exit)
+__device__ int worker_claim(CoopCtl* cc, uint32_t* idx) {
+  const unsigned long long t0 = wall_clock64();
+  for (uint32_t spin = 0;; ++spin) {
+    const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
+    if (cn < hn) {
+      if (w_cas(&cc->claim_n, cn, cn + 1u)) {
+        *idx = cn;
+        return 0;
+      }
+      continue;
+    }
+    if (__hip_atomic_load(&cc->stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+      // the final needed head was published before `stop`: drain what is left, then exit
+      if (w_ld(&cc->claim_n) < w_ld(&cc->head_n)) continue;
+      return -1;
+    }
+    const uint32_t hs = w_ld(&cc->head_s), cs = w_ld(&cc->claim_s);
+    if (cs < hs) {
+      if (w_cas(&cc->claim_s, cs, cs + 1u)) {
+        *idx = cs;
+        return 1;
+      }
+      continue;
+    }
+    if (wall_clock64() - t0 > 500000000ull) return -1;  // 5 s idle: safety exit
+    if (spin < 256) __builtin_amdgcn_s_sleep(2);
+    else __builtin_amdgcn_s_sleep(16);
+  }
+}
+
+// global g-score slot tag (k_astar / tier-2 scheme: tag:10 | label:2 | g:20, cleared every 1023)
+__device__ __forceinline__ uint32_t slot_tag(uint32_t* GS, uint32_t ncell, uint32_t& ep, uint32_t lane) {
+  if (ep % 1023u == 0u && ep > 0u) {
+    for (uint32_t c = lane; c < ncell; c += 64u) GS[c] = 0u;
+    __threadfence_block();
+  }
+  __syncthreads();
+  const uint32_t tag = ep % 1023u + 1u;
+  ++ep;
+  return tag;
+}
+
+__global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
+  extern __shared__ __align__(16) uint64_t wsm[];
+  const DevGrid G = A.G;
+  uint64_t* Hp = wsm;
+  const uint32_t lane = threadIdx.x, ncell = G.ncell, hcap = A.hcap, gs_lds = A.gs_lds;
+  uint32_t* GSl = reinterpret_cast<uint32_t*>(wsm + hcap);  // gs_lds == 1
+  uint8_t* GB = reinterpret_cast<uint8_t*>(wsm + hcap);      // gs_lds == 2
+  const uint32_t gsb = gs_lds == 1u ? ncell * 4u : gs_lds == 2u ? (ncell + 15u) / 16u * 16u : 0u;
+  uint32_t* FB = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wsm + hcap) + gsb);
+  const uint32_t nfw = G.H * G.Ww;
+  for (uint32_t t = lane; t < nfw; t += 64u) FB[t] = G.freebits[t];
+  if (gs_lds == 1u)
+    for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
+  uint32_t* GSg = A.gs_all + (uint64_t)blockIdx.x * ncell;
+  uint64_t* Hg = A.heaps + (uint64_t)blockIdx.x * A.ghcap;
+  uint32_t ep = A.epochs[blockIdx.x], epl = 0;
+  __syncthreads();
+  if (lane == 0) __hip_atomic_fetch_add(&A.cc->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    int which = -1;
+    uint32_t idx = 0;
+    if (lane == 0) which = worker_claim(A.cc, &idx);
+    which = __builtin_amdgcn_readfirstlane(which);
+    if (which < 0) break;
+    idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+    // the entry was published by the planner's release of the head: read it past stale caches
+    const uint32_t* e = reinterpret_cast<const uint32_t*>((which ? A.QS : A.QN) + idx);
+    const uint32_t v = w_ld(e), goal = w_ld(e + 1);
+    const int32_t tab = (int32_t)w_ld(e + 2);
+    int32_t L = 0;
+    uint8_t code = NH_UNKNOWN;
+    // tier 1: LDS heap, g-scores in LDS (bytes or u32) or in the global slot
+    if (gs_lds == 2u) {
+      uint4* g4 = reinterpret_cast<uint4*>(GB);
+      for (uint32_t c = lane; c < (ncell + 15u) / 16u; c += 64u) g4[c] = make_uint4(0u, 0u, 0u, 0u);
+      __syncthreads();
+      code = astar_wave_par<2, false>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr);
+    } else if (gs_lds == 1u) {
+      if (epl % 1023u == 0u && epl > 0u) {
+        for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
+      }
+      __syncthreads();
+      const uint32_t tag = epl % 1023u + 1u;
+      ++epl;
+      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr);
+    } else {
+      const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
+      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr);
+    }
+    // tier 2: byte / LDS g-scores outgrew their encoding -> u32 g-scores in the global slot
+    if (L == -2 && gs_lds != 0u) {
+      const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
+      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr);
+    }
+    // tier 3: the LDS heap overflowed -> lone-lane A* with the heap in the global slot
+    if (L == -2) {
+      const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
+      if (lane == 0) code = astar_one(G, v, goal, tag, Hg, A.ghcap, GSg, &L, &A.cc->err);
+      code = (uint8_t)__builtin_amdgcn_readfirstlane(code);
+    }
+    if (lane == 0 && tab >= 0) {
+      // the code (or NH_UNKNOWN after a global-heap overflow, flagged in cc->err) — an agent-scope
+      // store the planner's polling load sees
+      uint8_t* dst = A.nh + (uint64_t)tab * A.nstride + v;
+      __hip_atomic_store(dst, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&A.cc->worker_queries, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (lane == 0) A.epochs[blockIdx.x] = ep;
+}
+
+uint32_t worker_waves(const DevGrid& G, int num_cu) { return astar_wave_slots(G, num_cu, false); }
+
+hipError_t launch_astar_workers(const WorkerArgs& A0, uint32_t waves, hipStream_t s) {
+  WorkerArgs A = A0;
+  A.gs_lds = wave_gs_mode(A.G);
+  A.hcap = wave_fit_hcap(A.G, A.hcap ? std::min(A.hcap, WAVE_HCAP) : WAVE_HCAP, A.gs_lds);
+  if (A.hcap < 4u || waves == 0) return hipErrorInvalidValue;
+  const size_t lds = wave_lds_bytes(A.G, A.hcap, A.gs_lds);
+  hipError_t e = hipFuncSetAttribute((const void*)k_astar_worker, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_astar_worker, dim3(waves), dim3(64), lds, s, A);
   return hipGetLastError();
 }
 

@@ -76,6 +76,13 @@ struct PlanArgs {
   PlanCtl* ctl;
   unsigned long long* sec_ticks;  // [16] wall-clock ticks per section [0..7] and sub-phase [8..15] (diagnostics)
   uint32_t dbg;                   // sub-phase ticks on (TSW_PLAN_DEBUG)
+  // coop mode: K3 runs concurrently in k_astar_worker; Q is the needed queue (qcap entries for the
+  // whole launch), QS the speculative one; missing next hops are waited for instead of exiting
+  uint32_t coop;
+  AstarQuery* QS;
+  uint32_t qscap;
+  CoopCtl* cc;
+  uint32_t* started;              // host-visible: set when the planner block is resident
 };
 
 // flinks: the pointer-doubling buffers F1/F2 alone in LDS (when the agent arrays are not)
@@ -83,5 +90,25 @@ size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool 
 hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, uint32_t* dups,
                       hipStream_t s);
 hipError_t launch_plan(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s);
+
+// Persistent K3 worker waves for coop mode (tsw_kernels.hip): claim queued pairs from cc's queues
+// (needed first), resolve them with the exact A* and write the next-hop code; exit when the planner
+// has stopped and the needed queue is drained (speculative leftovers are abandoned).
+struct WorkerArgs {
+  DevGrid G;
+  CoopCtl* cc;
+  const AstarQuery* QN;
+  const AstarQuery* QS;
+  uint8_t* nh;
+  uint64_t nstride;
+  uint32_t hcap;      // LDS heap entries
+  uint32_t gs_lds;    // 0: u32 g-scores in the global slots, 1: u32 in LDS, 2: bytes in LDS
+  uint32_t* gs_all;   // per-wave global g-score slots (tier 2 / tier 3), ncell u32 each
+  uint32_t* epochs;   // per-slot tag epochs
+  uint64_t* heaps;    // per-wave global heaps (tier 3), ghcap entries each
+  uint32_t ghcap;
+};
+uint32_t worker_waves(const DevGrid& G, int num_cu);
+hipError_t launch_astar_workers(const WorkerArgs& A, uint32_t waves, hipStream_t s);
 
 }  // namespace tsw

@@ -178,22 +178,44 @@ __device__ __forceinline__ void put_query(const PlanArgs& P, uint8_t* p, uint32_
   P.Q[qi] = q;
 }
 
-// A pair a step needs now (the planner exits for K3 right after): queue it if it is unresolved.
-// Needed pairs are at most 2n per exit and the speculative ones stay below qcap/2, so the queue
-// (qcap = 4n + 4096) cannot overflow; if it ever did, the pair is not marked and the host, seeing
-// qcount > qcap, fails the call.
+// A pair a step needs now: queue it if it is unresolved (the planner then exits for a host-side K3
+// pass, or — coop mode — waits for the concurrent workers). Needed pairs are at most 2n per exit and
+// the speculative ones stay below qcap/2, so the queue (qcap = 4n + 4096) cannot overflow; if it
+// ever did, the pair is not marked and the host, seeing qcount > qcap, fails the call. In coop mode
+// a pair already queued speculatively is promoted: queued again on the needed queue, which the
+// workers serve first (the duplicate resolves to the same code).
+// s_q[0]: needed pairs queued since the launch began, s_q[1]: speculative ones (coop mode).
 __device__ __forceinline__ void enqueue_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q) {
   uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
-  if (*p != NH_UNKNOWN) return;  // PENDING: whoever flipped it enqueued it in this pass
-  const uint32_t qi = atomicAdd(s_q, 1u);
+  const uint8_t c = *p;
+  if (c != NH_UNKNOWN && !(P.coop && c == NH_PENDING_S)) return;  // queued (PENDING) or resolved
+  const uint32_t qi = atomicAdd(&s_q[0], 1u);
   if (qi < P.qcap) put_query(P, p, qi, v, g, tab);
 }
 
-// A speculative prefetch: the slot is reserved by CAS only while the queue holds fewer than
-// qcap/2 pairs, so prefetches never take the room the needed pairs of an exit rely on.
+// speculative queue full (no more prefetches this launch)
+__device__ __forceinline__ bool spec_full(const PlanArgs& P, const uint32_t* s_q) {
+  return P.coop ? *(volatile const uint32_t*)&s_q[1] >= P.qscap : *(volatile const uint32_t*)&s_q[0] >= P.qcap / 2u;
+}
+
+// A speculative prefetch. Exit mode: the slot is reserved by CAS only while the queue holds fewer
+// than qcap/2 pairs, so prefetches never take the room the needed pairs of an exit rely on. Coop
+// mode: its own queue (QS), resolved by the workers after every needed pair.
 __device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q) {
   uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
   if (*p != NH_UNKNOWN) return;
+  if (P.coop) {
+    const uint32_t qi = atomicAdd(&s_q[1], 1u);
+    if (qi >= P.qscap) return;
+    *p = NH_PENDING_S;
+    AstarQuery q;
+    q.v = v;
+    q.goal = g;
+    q.tab = tab;
+    q.out = qi;
+    P.QS[qi] = q;
+    return;
+  }
   const uint32_t lim = P.qcap / 2u;
   uint32_t cur = *(volatile uint32_t*)s_q;
   for (;;) {
@@ -234,6 +256,115 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
   return *s_need;
 }
 
+// ---- coop mode (concurrent K3 workers) ------------------------------------------------------
+// Memory: the planner's queue entries and PENDING marks are plain stores published by one release
+// store of the queue heads (agent scope: written back past this XCD's L2); workers read entries with
+// agent-scope loads and write each code with an agent-scope store, which the planner polls with
+// agent-scope loads. A code, once written, never changes, so a stale plain read of the table can
+// only see an older state (UNKNOWN / PENDING) — a conservative "unresolved", never a wrong hop.
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// thread 0: make every entry queued so far visible to the workers (caller: after a barrier)
+__device__ __forceinline__ void coop_publish(const PlanArgs& P, const uint32_t* s_q) {
+  const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap);
+  __hip_atomic_store(&P.cc->head_s, hs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&P.cc->head_n, hn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr unsigned long long COOP_NO_WORKER_TICKS = 5000000ull;  // 50 ms at 100 MHz: workers never started
+constexpr unsigned long long COOP_RETRY_TICKS = 2000000ull;      // 20 ms pending: queue the pair again
+constexpr unsigned long long COOP_GIVE_UP_TICKS = 500000000ull;  // 5 s: safety valve
+enum : int { COOP_OK = 0, COOP_GIVE_UP = 1, COOP_RETRY = 2 };
+
+// Parallel (block-uniform result): publish, then wait until every agent whose next-hop code is dirty
+// has it or is no longer pending (UNKNOWN: not queued — the caller's refresh queues it). Codes read
+// here go straight into the agent's NHC. COOP_GIVE_UP: no worker alive, a worker error, or the
+// safety limit (the caller exits to the host). COOP_RETRY: a pair stayed pending for 20 ms — more
+// than any A* on these grids; the caller queues the still-pending pairs again (a duplicate query
+// resolves to the same code), so a lost update can cost a retry but never a stall.
+__device__ int coop_wait(const PlanArgs& P, const Arrays& S, const uint32_t* s_q, uint32_t* s_flag) {
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  if (tid == 0) {
+    coop_publish(P, s_q);
+    *s_flag = COOP_OK;
+  }
+  __syncthreads();
+  const unsigned long long t0 = wall_clock64();
+  int st = COOP_OK;
+  for (uint32_t k = tid; k < P.n && st == COOP_OK; k += bd) {
+    if (S.NHC[k] <= NH_STAY) continue;
+    const uint32_t v = S.V[k];
+    const int32_t tab = S.GT[k];
+    if (v == S.G[k] || tab < 0) continue;
+    const uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u);
+    const uint32_t sh = 8u * (uint32_t)((uintptr_t)p & 3u);
+    for (uint32_t spin = 0;; ++spin) {
+      const uint8_t c = (uint8_t)(ld_agent(w) >> sh);
+      if (c <= NH_STAY) {
+        S.NHC[k] = c;
+        break;
+      }
+      if (c == NH_UNKNOWN) break;
+      const unsigned long long dt = wall_clock64() - t0;
+      if (dt > COOP_GIVE_UP_TICKS || ld_agent(&P.cc->err) != 0u ||
+          (dt > COOP_NO_WORKER_TICKS && ld_agent(&P.cc->alive) == 0u)) {
+        st = COOP_GIVE_UP;
+        break;
+      }
+      if (dt > COOP_RETRY_TICKS) {
+        st = COOP_RETRY;
+        break;
+      }
+      if (spin < 64) __builtin_amdgcn_s_sleep(1);
+      else __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  if (st != COOP_OK) atomicMax(s_flag, (uint32_t)(st == COOP_GIVE_UP ? 3 : st));
+  __syncthreads();
+  const uint32_t f = *s_flag;
+  if (tid == 0) {
+    P.cc->waits += 1u;
+    P.cc->wait_ticks += wall_clock64() - t0;
+  }
+  __syncthreads();
+  return f == 3u ? COOP_GIVE_UP : (int)f;
+}
+
+// COOP_RETRY: every dirty agent whose pair still reads pending is queued again on the needed queue
+__device__ void coop_requeue(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
+  for (uint32_t k = tid; k < P.n; k += bd) {
+    if (S.NHC[k] <= NH_STAY) continue;
+    const uint32_t v = S.V[k];
+    const int32_t tab = S.GT[k];
+    if (v == S.G[k] || tab < 0) continue;
+    uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u);
+    const uint8_t c = (uint8_t)(ld_agent(w) >> (8u * (uint32_t)((uintptr_t)p & 3u)));
+    if (c != NH_PENDING && c != NH_PENDING_S) continue;
+    const uint32_t qi = atomicAdd(&s_q[0], 1u);
+    if (qi < P.qcap) put_query(P, p, qi, v, S.G[k], tab);
+  }
+  __syncthreads();
+}
+
+// Next hops are missing (refresh_codes returned nonzero and queued them). Coop mode: wait for the
+// workers and re-run the refresh until nothing is missing (true: continue in the kernel). Otherwise,
+// or if the workers do not answer, false: the caller exits for a host-side K3 pass.
+__device__ bool coop_resolve(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need, uint32_t* s_flag) {
+  if (!P.coop) return false;
+  for (int it = 0; it < 1024; ++it) {
+    const int st = coop_wait(P, S, s_q, s_flag);
+    if (st == COOP_GIVE_UP) return false;
+    if (st == COOP_RETRY) coop_requeue(P, S, s_q);
+    if (refresh_codes(P, S, s_q, s_need) == 0u) return true;
+  }
+  return false;
+}
+
 // Parallel, after rules_init: the next hops a firing of this rules round (or the movement phase
 // after it) could need. A rule-3
 // swap hands succ(k) the goal of k (tswap.rs:199-202); a rule-4 rotation hands every cycle
@@ -245,7 +376,7 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
 __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t k = tid; k < P.n; k += bd) {
-    if (*(volatile uint32_t*)s_q >= P.qcap / 2u) break;
+    if (spec_full(P, s_q)) break;
     const int32_t tab = S.GT[k];
     if (tab < 0) continue;
     // k's own next hop from the cell it moves to: read by the movement phase when k moved
@@ -272,7 +403,7 @@ __device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t
                                     uint32_t cnt) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t i = tid; i < cnt; i += bd) {
-    if (*(volatile uint32_t*)s_q >= P.qcap / 2u) break;
+    if (spec_full(P, s_q)) break;
     const uint32_t k = lst[i];
     const int32_t tab = S.GT[k];
     if (tab < 0) continue;
@@ -295,7 +426,7 @@ __device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t
 __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x, hops = P.wide_prefetch ? P.wide_prefetch : 1u;
   for (uint32_t k = tid; k < P.n; k += bd) {
-    if (*(volatile uint32_t*)s_q >= P.qcap / 2u) break;
+    if (spec_full(P, s_q)) break;
     // heading to a pickup: the pair the state machine needs on arrival (goal := delivery,
     // tswap.rs:113-118) is known since the assignment — (pickup cell, delivery goal)
     if (P.mode != MODE_STEP && P.m > 0 && P.st[k] == ST_TO_PICKUP) {
@@ -389,7 +520,7 @@ template <bool AG, bool OC>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q, s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss;
+  __shared__ uint32_t s_q[2], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[16], s_tlast, s_tp;
@@ -471,19 +602,25 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_ctl = *P.ctl;
     s_ctl.status = PLAN_RUNNING;
     s_exit = 0;
-    s_q = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
+    s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
+    s_q[1] = 0;  // speculative queue (coop mode)
     for (int k = 0; k < 16; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
+    // coop mode: tell the host the planner is resident, so the workers it launches next cannot
+    // take the CUs this block needs
+    if (P.started) __hip_atomic_store(P.started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
   if (s_ctl.section == SEC_RULES || s_ctl.section == SEC_MOVE) {
     // resuming after K3 resolved the missing next hops: every code starts dirty here
-    const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
-    if (q > 0 && tid == 0) {
-      s_ctl.qcount = s_q;
-      s_ctl.status = PLAN_NEED_QUERIES;
-      s_exit = 1;
+    const uint32_t q = refresh_codes(P, S, s_q, &s_need);
+    if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag)) {
+      if (tid == 0) {
+        s_ctl.qcount = s_q[0];
+        s_ctl.status = PLAN_NEED_QUERIES;
+        s_exit = 1;
+      }
     }
     __syncthreads();
   }
@@ -589,13 +726,14 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       }
       __syncthreads();
     } else if (sec == SEC_PRE1 || sec == SEC_PRE2) {
-      const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
+      const uint32_t q = refresh_codes(P, S, s_q, &s_need);
       // step start: queue every agent's next hop from the cell it is about to enter now, so
       // the assignment exit's K3 batch (if any) already carries what the movement phase reads
-      if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, &s_q);
-      if (q > 0) {
+      if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, s_q);
+      if (P.coop && tid == 0) coop_publish(P, s_q);  // speculative pairs start resolving now
+      if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag)) {
         if (tid == 0) {
-          s_ctl.qcount = s_q;
+          s_ctl.qcount = s_q[0];
           s_ctl.status = PLAN_NEED_QUERIES;
           s_exit = 1;
         }
@@ -617,7 +755,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // candidate k, so a swap needs no global round trip on the serial path.
       if (P.dbg && tid == 0) s_tp = wall_clock64();
       rules_init(P, S);
-      if (P.prefetch) rules_prefetch(P, S, &s_q);
+      if (P.prefetch) rules_prefetch(P, S, s_q);
+      if (P.coop && tid == 0) coop_publish(P, s_q);
       if (tid == 0) s_cnt = 0;
       PLAN_TICK(15);
       // One firing agent per round (tswap.rs:180-252 in agent order): fire(b) applies b's rule 3
@@ -833,10 +972,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (s_best == NO_AGENT) break;
         if (s_miss) {
           // goals of the fired agents changed: their next hops (hence succ) must be looked up
-          const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
-          if (q > 0) {
+          const uint32_t q = refresh_codes(P, S, s_q, &s_need);
+          if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag)) {
             if (tid == 0) {
-              s_ctl.qcount = s_q;
+              s_ctl.qcount = s_q[0];
               s_ctl.status = PLAN_NEED_QUERIES;
               s_exit = 1;
             }
@@ -845,8 +984,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           }
           rules_init(P, S);
           if (P.prefetch) {
-            if (P.wide_prefetch && s_cnt != NO_AGENT) rules_prefetch_list(P, S, &s_q, list, s_cnt);
-            else rules_prefetch(P, S, &s_q);
+            if (P.wide_prefetch && s_cnt != NO_AGENT) rules_prefetch_list(P, S, s_q, list, s_cnt);
+            else rules_prefetch(P, S, s_q);
+            if (P.coop && tid == 0) coop_publish(P, s_q);
           }
           if (tid == 0) s_cnt = 0;
           PLAN_TICK(15);
@@ -869,10 +1009,15 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       }
       __syncthreads();
       if (s_ctl.miss) {
-        const uint32_t q = refresh_codes(P, S, &s_q, &s_need);
+        const uint32_t q = refresh_codes(P, S, s_q, &s_need);
+        if (s_ctl.miss == 1 && q > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag)) {
+          if (tid == 0) s_ctl.miss = 0;
+          __syncthreads();
+          continue;  // resume the serial scan at ctl.i
+        }
         if (tid == 0) {
-          s_ctl.qcount = s_q;
-          s_ctl.status = (q > 0 && s_q > 0 && s_ctl.miss == 1) ? PLAN_NEED_QUERIES : PLAN_ERROR;
+          s_ctl.qcount = s_q[0];
+          s_ctl.status = (q > 0 && s_q[0] > 0 && s_ctl.miss == 1) ? PLAN_NEED_QUERIES : PLAN_ERROR;
           s_exit = 1;
         }
         __syncthreads();
@@ -895,7 +1040,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         const int code = lookup_code(P, S, k);
         if (code < 0) {
           if (code == -2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
-          else enqueue_pair(P, S.V[k], S.G[k], S.GT[k], &s_q);
+          else enqueue_pair(P, S.V[k], S.G[k], S.GT[k], s_q);
           s_miss = 1;
           S.SUCC[k] = NO_CELL;
           return true;
@@ -945,7 +1090,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
               const int cj = lookup_code(P, S, j);
               if (cj < 0) {
                 if (cj == -2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
-                else enqueue_pair(P, S.V[j], S.G[j], S.GT[j], &s_q);
+                else enqueue_pair(P, S.V[j], S.G[j], S.GT[j], s_q);
                 s_miss = 1;
                 return;
               }
@@ -1058,9 +1203,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         __syncthreads();
       }
       if (s_miss) {
+        // the missing codes are queued (pass 1 / pass 2) and their agents' codes are dirty
+        if (s_q[0] > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag)) continue;  // replay the open rounds
         if (tid == 0) {
-          s_ctl.qcount = s_q;
-          s_ctl.status = s_q > 0 ? PLAN_NEED_QUERIES : PLAN_ERROR;
+          s_ctl.qcount = s_q[0];
+          s_ctl.status = s_q[0] > 0 ? PLAN_NEED_QUERIES : PLAN_ERROR;
           s_exit = 1;
         }
         __syncthreads();
@@ -1076,7 +1223,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (tid == 0) {
           s_ctl.status = PLAN_DONE;
           s_ctl.section = SEC_DONE;
-          s_ctl.qcount = s_q;  // speculative prefetches still queued: the host resolves them
+          s_ctl.qcount = s_q[0];  // speculative prefetches still queued: the host resolves them
           s_exit = 1;
         }
         __syncthreads();
@@ -1105,7 +1252,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if ((s_ctl.unused == 0u && !busy) || s_ctl.t > s_ctl.max_t) {
           s_ctl.status = PLAN_DONE;
           s_ctl.section = SEC_DONE;
-          s_ctl.qcount = s_q;  // speculative prefetches still queued: the host resolves them
+          s_ctl.qcount = s_q[0];  // speculative prefetches still queued: the host resolves them
           s_exit = 1;
         } else {
           s_ctl.section = SEC_ASSIGN;
@@ -1128,6 +1275,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   if constexpr (OC)
     for (uint32_t c = tid; c < P.ncell; c += bd) P.occ[c] = S.OCC[c];
   if (tid == 0) {
+    if (P.coop) {  // last publish, then release the workers (they drain the needed queue and exit)
+      coop_publish(P, s_q);
+      __hip_atomic_store(&P.cc->stop, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const uint32_t err = P.ctl->err;
     *P.ctl = s_ctl;
     P.ctl->err |= err;
