@@ -198,6 +198,8 @@ typedef struct {
      * a worker, and its total waiting time (inside walker_ms) */
     uint64_t coop_waits;
     double coop_wait_ms;
+    double coop_wait_sec_ms[8]; /* ... by planner section (plan_section_ms indices) */
+    uint64_t coop_waits_sec[8];
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

@@ -89,12 +89,15 @@ class Stats(ctypes.Structure):
         ("plan_section_ms", ctypes.c_double * 8), ("rule_rounds", ctypes.c_uint64),
         ("plan_exits", ctypes.c_uint64 * 8), ("table_evictions", ctypes.c_uint64),
         ("coop_waits", ctypes.c_uint64), ("coop_wait_ms", ctypes.c_double),
+        ("coop_wait_sec_ms", ctypes.c_double * 8), ("coop_waits_sec", ctypes.c_uint64 * 8),
     ]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
         d["plan_section_ms"] = list(self.plan_section_ms)
         d["plan_exits"] = list(self.plan_exits)
+        d["coop_wait_sec_ms"] = list(self.coop_wait_sec_ms)
+        d["coop_waits_sec"] = list(self.coop_waits_sec)
         return d
 
 

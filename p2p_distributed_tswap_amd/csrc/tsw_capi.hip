@@ -64,6 +64,7 @@ struct Tunables {
   uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
+  bool task_chains = true;        // TSW_TASK_CHAINS=0: no task-chain jobs for the coop workers
 
   static Tunables from_env() {
     Tunables t;
@@ -90,6 +91,7 @@ struct Tunables {
     t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
+    t.task_chains = num("TSW_TASK_CHAINS", 0, 1, 1) != 0;
     return t;
   }
 };
@@ -164,6 +166,9 @@ struct tsw_ctx {
   CoopCtl* h_cc = nullptr;       // pinned
   AstarQuery* d_QS = nullptr;
   size_t qscap = 0;
+  AstarQuery* d_QT = nullptr;    // task chains of the current plan (host-filled)
+  size_t qtcap = 0;
+  uint32_t qt_count = 0;
   uint32_t* h_started = nullptr; // pinned, coherent: set by the planner block when resident
   uint32_t* d_started = nullptr;
 
@@ -997,31 +1002,41 @@ int build_occ(tsw_ctx* c, uint32_t n) {
 int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   *c->h_ctl = init;
   HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
-  const size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds);
+  size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds);
+  // coop mode: the planner block reserves its CU's whole LDS so no worker wave is placed beside it
+  // (they would compete for its SIMDs and LDS bandwidth on the critical path)
+  if (P.coop) lds = std::max<size_t>(lds, (size_t)std::max(c->max_lds - 2048, 0));
   // one lane per agent in the parallel passes when possible; >= 4 waves for the task argmin
   uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
   if (c->tun.plan_block) block = std::max<uint32_t>(64u, c->tun.plan_block);
   const bool coop = P.coop != 0;
   WorkerArgs W{};
-  uint32_t waves = 0;
+  WorkerCfg wcfg{};
   if (coop) {
     W.G = c->G;
     W.cc = c->d_cc;
     W.QN = c->d_Q;
     W.QS = c->d_QS;
+    W.QT = c->d_QT;
     W.nh = c->d_nh;
     W.nstride = c->tstride;
     W.hcap = c->tun.wave_hcap;
+    // task chains take half the workers at most (a quarter with many agents: their needed bursts
+    // are larger), the rest stay free for the pairs the planner waits on
+    W.tmask = P.n > 2000u ? 3u : 1u;
     W.gs_all = c->d_gs;
     W.epochs = c->d_epochs;
     W.heaps = c->d_heaps;
     W.ghcap = c->hcap;
-    waves = std::min(worker_waves(c->G, c->num_cu), c->nslots);
+    wcfg = worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap);
+    wcfg.waves = std::min(wcfg.waves, c->nslots);
   }
   for (uint64_t round = 0;; ++round) {
     if (round > 16ull * P.n + 4096ull * (init.max_t + 1)) RET(TSW_EINVAL, "plan kernel made no progress");
     if (coop) {
       HIPCHK(hipMemsetAsync(c->d_cc, 0, sizeof(CoopCtl), c->s));
+      const uint32_t nt = P.mode == MODE_MAPD ? c->qt_count : 0u;
+      if (nt) HIPCHK(hipMemcpyAsync(&c->d_cc->head_t, &c->qt_count, 4, hipMemcpyHostToDevice, c->s));
       *(volatile uint32_t*)c->h_started = 0u;
     }
     {
@@ -1037,7 +1052,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       while (!*(volatile uint32_t*)c->h_started &&
              std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500)) {
       }
-      HIPCHK(launch_astar_workers(W, waves, c->s2));
+      HIPCHK(launch_astar_workers(W, wcfg, c->s2));
       c->st.astar_launches++;
     }
     HIPCHK(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(PlanCtl), hipMemcpyDeviceToHost, c->s));
@@ -1048,6 +1063,10 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       const CoopCtl& cc = *c->h_cc;
       c->st.coop_waits += cc.waits;
       c->st.coop_wait_ms += (double)cc.wait_ticks / (double)c->wall_khz;
+      for (int k = 0; k < 8; ++k) {
+        c->st.coop_wait_sec_ms[k] += (double)cc.wait_sec[k] / (double)c->wall_khz;
+        c->st.coop_waits_sec[k] += cc.waits_sec[k];
+      }
       c->st.astar_queries += cc.worker_queries;
       if (cc.err) RET(TSW_EOVERFLOW, "K3 worker: A* heap overflow");
       // speculative pairs nobody claimed stay PENDING_S: back to UNKNOWN for later calls
@@ -1161,7 +1180,27 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   TRY(build_occ(c, n));
   TRY(ensure_tables(c, goalset));
   TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
-  if (c->tun.coop && !eager_policy(c, 0)) TRY(ensure_coop(c, n));
+  c->qt_count = 0;
+  if (c->tun.coop && !eager_policy(c, 0)) {
+    TRY(ensure_coop(c, n));
+    if (c->tun.task_chains && m) {
+      // every task's pickup -> delivery path, resolved hop by hop by the workers in the background
+      // (lowest priority): an agent that picks the task up finds its next hops already there
+      std::vector<AstarQuery> qt;
+      qt.reserve(m);
+      for (uint32_t k = 0; k < m; ++k)
+        if (pick[k] != dlv[k]) qt.push_back(AstarQuery{pick[k], dlv[k], c->h_goal_tab[dlv[k]], 0u});
+      if (qt.size() > c->qtcap) {
+        HIPCHK(hipStreamSynchronize(c->s));
+        HIPCHK(dgrow(c->d_QT, c->qtcap, qt.size()));
+      }
+      if (!qt.empty()) {
+        HIPCHK(hipMemcpyAsync(c->d_QT, qt.data(), qt.size() * sizeof(AstarQuery), hipMemcpyHostToDevice, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+      }
+      c->qt_count = (uint32_t)qt.size();
+    }
+  }
   PlanArgs P = plan_args(c, n, m, MODE_MAPD, goal_out != nullptr);
   PlanCtl init{};
   init.section = SEC_ASSIGN;
@@ -1350,7 +1389,7 @@ void tsw_destroy(tsw_ctx* c) {
   if (c->h_dups) (void)hipHostFree(c->h_dups);
   fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
-  fre(c->d_cc); fre(c->d_QS);
+  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_started) (void)hipHostFree(c->h_started);
   if (c->s2) (void)hipStreamDestroy(c->s2);

@@ -60,10 +60,15 @@ struct CoopCtl {
   uint32_t claim_n, pad1[31];  // needed queue: entries claimed by workers
   uint32_t head_s, pad2[31];   // speculative queue: published
   uint32_t claim_s, pad3[31];  // speculative queue: claimed
+  uint32_t head_t, pad5[31];   // task-chain queue (filled by the host before the launch)
+  uint32_t claim_t, pad6[31];  // task-chain queue: claimed
   uint32_t stop, alive, err, waits;  // planner finished / workers started / worker error bits / planner waits
   unsigned long long wait_ticks;     // planner time spent waiting on workers (100 MHz ticks)
   unsigned long long worker_queries; // queries resolved by workers
-  uint32_t pad4[24];
+  unsigned long long chain_queries;  // ... of which on task chains
+  unsigned long long wait_sec[8];    // wait ticks by planner section (SEC_*)
+  uint32_t waits_sec[8];             // waits by planner section
+  uint32_t pad4[2];
 };
 
 struct AstarQuery {

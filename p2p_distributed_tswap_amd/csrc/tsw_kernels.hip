@@ -1220,8 +1220,10 @@ __device__ __forceinline__ bool w_cas(uint32_t* p, uint32_t expect, uint32_t wan
                                               __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// lane 0: claim the next pair (0: needed queue, 1: speculative queue, -1: exit)
-__device__ int worker_claim(CoopCtl* cc, uint32_t* idx) {
+// lane 0: claim the next pair (0: needed queue, 1: speculative queue, 2: task chain, -1: exit).
+// Task chains (long, lowest priority) only go to workers with take_t: the others stay free for the
+// pairs the planner needs or will need soon.
+__device__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t) {
   const unsigned long long t0 = wall_clock64();
   for (uint32_t spin = 0;; ++spin) {
     const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
@@ -1232,7 +1234,9 @@ __device__ int worker_claim(CoopCtl* cc, uint32_t* idx) {
       }
       continue;
     }
-    if (__hip_atomic_load(&cc->stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+    // relaxed poll (an acquire here would invalidate this XCD's L2 on every idle spin)
+    if (w_ld(&cc->stop)) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
       // the final needed head was published before `stop`: drain what is left, then exit
       if (w_ld(&cc->claim_n) < w_ld(&cc->head_n)) continue;
       return -1;
@@ -1244,6 +1248,16 @@ __device__ int worker_claim(CoopCtl* cc, uint32_t* idx) {
         return 1;
       }
       continue;
+    }
+    if (take_t) {
+      const uint32_t ht = w_ld(&cc->head_t), ct = w_ld(&cc->claim_t);
+      if (ct < ht) {
+        if (w_cas(&cc->claim_t, ct, ct + 1u)) {
+          *idx = ct;
+          return 2;
+        }
+        continue;
+      }
     }
     if (wall_clock64() - t0 > 500000000ull) return -1;  // 5 s idle: safety exit
     if (spin < 256) __builtin_amdgcn_s_sleep(2);
@@ -1271,9 +1285,13 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
   uint32_t* GSl = reinterpret_cast<uint32_t*>(wsm + hcap);  // gs_lds == 1
   uint8_t* GB = reinterpret_cast<uint8_t*>(wsm + hcap);      // gs_lds == 2
   const uint32_t gsb = gs_lds == 1u ? ncell * 4u : gs_lds == 2u ? (ncell + 15u) / 16u * 16u : 0u;
-  uint32_t* FB = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wsm + hcap) + gsb);
-  const uint32_t nfw = G.H * G.Ww;
-  for (uint32_t t = lane; t < nfw; t += 64u) FB[t] = G.freebits[t];
+  const uint32_t* FB = G.freebits;
+  if (A.stage_fb) {
+    uint32_t* fb = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wsm + hcap) + gsb);
+    const uint32_t nfw = G.H * G.Ww;
+    for (uint32_t t = lane; t < nfw; t += 64u) fb[t] = G.freebits[t];
+    FB = fb;
+  }
   if (gs_lds == 1u)
     for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
   uint32_t* GSg = A.gs_all + (uint64_t)blockIdx.x * ncell;
@@ -1281,20 +1299,11 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
   uint32_t ep = A.epochs[blockIdx.x], epl = 0;
   __syncthreads();
   if (lane == 0) __hip_atomic_fetch_add(&A.cc->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (;;) {
-    int which = -1;
-    uint32_t idx = 0;
-    if (lane == 0) which = worker_claim(A.cc, &idx);
-    which = __builtin_amdgcn_readfirstlane(which);
-    if (which < 0) break;
-    idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
-    // the entry was published by the planner's release of the head: read it past stale caches
-    const uint32_t* e = reinterpret_cast<const uint32_t*>((which ? A.QS : A.QN) + idx);
-    const uint32_t v = w_ld(e), goal = w_ld(e + 1);
-    const int32_t tab = (int32_t)w_ld(e + 2);
+  // exact A* for (v, goal): tier 1 LDS heap + LDS (or global) g-scores, tier 2 global u32
+  // g-scores, tier 3 global heap (the k_astar_wave -> k_astar hand-off chain, in one wave)
+  auto resolve = [&](uint32_t v, uint32_t goal) -> uint8_t {
     int32_t L = 0;
     uint8_t code = NH_UNKNOWN;
-    // tier 1: LDS heap, g-scores in LDS (bytes or u32) or in the global slot
     if (gs_lds == 2u) {
       uint4* g4 = reinterpret_cast<uint4*>(GB);
       for (uint32_t c = lane; c < (ncell + 15u) / 16u; c += 64u) g4[c] = make_uint4(0u, 0u, 0u, 0u);
@@ -1312,36 +1321,103 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
       code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr);
     }
-    // tier 2: byte / LDS g-scores outgrew their encoding -> u32 g-scores in the global slot
     if (L == -2 && gs_lds != 0u) {
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
       code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr);
     }
-    // tier 3: the LDS heap overflowed -> lone-lane A* with the heap in the global slot
     if (L == -2) {
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
       if (lane == 0) code = astar_one(G, v, goal, tag, Hg, A.ghcap, GSg, &L, &A.cc->err);
       code = (uint8_t)__builtin_amdgcn_readfirstlane(code);
     }
+    return code;
+  };
+  // the code (or NH_UNKNOWN after a global-heap overflow, flagged in cc->err): an agent-scope
+  // store the planner's polling load sees
+  auto publish_code = [&](uint32_t v, int32_t tab, uint8_t code, bool chain) {
     if (lane == 0 && tab >= 0) {
-      // the code (or NH_UNKNOWN after a global-heap overflow, flagged in cc->err) — an agent-scope
-      // store the planner's polling load sees
-      uint8_t* dst = A.nh + (uint64_t)tab * A.nstride + v;
-      __hip_atomic_store(dst, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(A.nh + (uint64_t)tab * A.nstride + v, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(&A.cc->worker_queries, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (chain) __hip_atomic_fetch_add(&A.cc->chain_queries, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  auto code_at = [&](uint32_t v, int32_t tab) -> uint8_t {  // current code, past stale caches
+    const uint8_t* p = A.nh + (uint64_t)tab * A.nstride + v;
+    const uint32_t w = w_ld(reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u));
+    return (uint8_t)(w >> (8u * (uint32_t)((uintptr_t)p & 3u)));
+  };
+  const bool take_t = (blockIdx.x & A.tmask) == A.tmask;
+  for (;;) {
+    int which = -1;
+    uint32_t idx = 0;
+    if (lane == 0) which = worker_claim(A.cc, &idx, take_t);
+    which = __builtin_amdgcn_readfirstlane(which);
+    if (which < 0) break;
+    idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+    // the entry was published by the planner's release of the head (or by the host before the
+    // launch): read it past stale caches
+    const uint32_t* e = reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : A.QT) + idx);
+    const uint32_t v = w_ld(e), goal = w_ld(e + 1);
+    const int32_t tab = (int32_t)w_ld(e + 2);
+    if (which < 2) {
+      publish_code(v, tab, resolve(v, goal), false);
+      continue;
+    }
+    // task chain: the path an agent carrying this task walks from its pickup to the delivery
+    // (every hop is get_path(cell, delivery)[1], tswap.rs:263-266): follow resolved codes and
+    // resolve each unresolved hop in turn; stop at a pair someone else has queued, at a stay code,
+    // or at the goal. Pairs are not marked pending, so an abandoned chain leaves nothing behind.
+    if (tab < 0) continue;
+    uint32_t c = v;
+    for (uint32_t hop = 0; hop < ncell && c != goal; ++hop) {
+      // the planner is done: abandon the rest of the chain (nothing is marked pending)
+      if ((uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? w_ld(&A.cc->stop) : 0u)) break;
+      uint8_t code = (uint8_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(c, tab) : 0u);
+      if (code == NH_UNKNOWN) {
+        code = resolve(c, goal);
+        publish_code(c, tab, code, true);
+      }
+      if (code >= NH_STAY) break;  // stay (unreachable goal), pending elsewhere, or overflow
+      c = step_cell(c, code, G.W);
     }
   }
   if (lane == 0) A.epochs[blockIdx.x] = ep;
 }
 
-uint32_t worker_waves(const DevGrid& G, int num_cu) { return astar_wave_slots(G, num_cu, false); }
+WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want) {
+  const size_t fbb = (size_t)G.H * G.Ww * 4u;
+  const uint32_t want = hcap_want ? std::min(hcap_want, WAVE_HCAP) : WAVE_HCAP;
+  auto make = [&](uint32_t m, bool fb) {
+    WorkerCfg c{};
+    c.gs_lds = m;
+    c.stage_fb = fb ? 1u : 0u;
+    const size_t gsb = m == 1u ? (size_t)G.ncell * 4u : m == 2u ? ((size_t)G.ncell + 15u) / 16u * 16u : 0u;
+    const size_t rest = gsb + (fb ? fbb : 0u);
+    c.hcap = rest < WAVE_LDS_MAX ? (uint32_t)std::min<size_t>(want, (WAVE_LDS_MAX - rest) / 8u) : 0u;
+    c.lds = (size_t)c.hcap * 8u + rest;
+    const uint32_t per_cu = c.lds ? (uint32_t)std::min<size_t>(16u, WAVE_LDS_MAX / c.lds) : 0u;
+    c.waves = (uint32_t)num_cu * per_cu;
+    return c;
+  };
+  const uint32_t m = wave_gs_mode(G);
+  WorkerCfg c = make(m, true);
+  // grids whose byte g-scores fit LDS (<= 120k cells): with many agents, trade the LDS g-scores for
+  // 3x the waves (global u32 slots, L2-resident at this size)
+  if (m != 0u && n_agents > 2000u && c.waves < 3u * (uint32_t)num_cu) c = make(0u, true);
+  // larger grids keep one wave per CU with the bitmap in LDS: their 4 MB g-score slots would not
+  // stay cache-resident with more waves, and the traffic slows the planner itself (C5: 3x)
+  if (c.hcap < 64u) c = make(0u, false);
+  return c;
+}
 
-hipError_t launch_astar_workers(const WorkerArgs& A0, uint32_t waves, hipStream_t s) {
+hipError_t launch_astar_workers(const WorkerArgs& A0, const WorkerCfg& cfg, hipStream_t s) {
   WorkerArgs A = A0;
-  A.gs_lds = wave_gs_mode(A.G);
-  A.hcap = wave_fit_hcap(A.G, A.hcap ? std::min(A.hcap, WAVE_HCAP) : WAVE_HCAP, A.gs_lds);
+  A.gs_lds = cfg.gs_lds;
+  A.stage_fb = cfg.stage_fb;
+  A.hcap = cfg.hcap;
+  const uint32_t waves = cfg.waves;
   if (A.hcap < 4u || waves == 0) return hipErrorInvalidValue;
-  const size_t lds = wave_lds_bytes(A.G, A.hcap, A.gs_lds);
+  const size_t lds = cfg.lds;
   hipError_t e = hipFuncSetAttribute((const void*)k_astar_worker, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_astar_worker, dim3(waves), dim3(64), lds, s, A);

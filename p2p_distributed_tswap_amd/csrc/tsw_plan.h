@@ -99,16 +99,26 @@ struct WorkerArgs {
   CoopCtl* cc;
   const AstarQuery* QN;
   const AstarQuery* QS;
+  const AstarQuery* QT;  // task chains: (pickup, delivery) of every task, walked hop by hop
   uint8_t* nh;
   uint64_t nstride;
   uint32_t hcap;      // LDS heap entries
   uint32_t gs_lds;    // 0: u32 g-scores in the global slots, 1: u32 in LDS, 2: bytes in LDS
+  uint32_t stage_fb;  // free-cell bitmap staged in LDS (else read from global memory / L2)
+  uint32_t tmask;     // workers with (blockIdx & tmask) == tmask also take task-chain jobs
   uint32_t* gs_all;   // per-wave global g-score slots (tier 2 / tier 3), ncell u32 each
   uint32_t* epochs;   // per-slot tag epochs
   uint64_t* heaps;    // per-wave global heaps (tier 3), ghcap entries each
   uint32_t ghcap;
 };
-uint32_t worker_waves(const DevGrid& G, int num_cu);
-hipError_t launch_astar_workers(const WorkerArgs& A, uint32_t waves, hipStream_t s);
+// Worker placement: per-wave LDS (heap, g-scores, free bitmap) sets the waves per CU. g-scores stay
+// in LDS (fastest per pop) unless that leaves < 3 waves per CU while many agents can need queries at
+// once (n > 2000): then they move to the global slots and more waves run.
+struct WorkerCfg {
+  uint32_t gs_lds, stage_fb, hcap, waves;
+  size_t lds;
+};
+WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want);
+hipError_t launch_astar_workers(const WorkerArgs& A, const WorkerCfg& cfg, hipStream_t s);
 
 }  // namespace tsw

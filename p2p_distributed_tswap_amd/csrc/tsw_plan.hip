@@ -284,7 +284,7 @@ enum : int { COOP_OK = 0, COOP_GIVE_UP = 1, COOP_RETRY = 2 };
 // safety limit (the caller exits to the host). COOP_RETRY: a pair stayed pending for 20 ms — more
 // than any A* on these grids; the caller queues the still-pending pairs again (a duplicate query
 // resolves to the same code), so a lost update can cost a retry but never a stall.
-__device__ int coop_wait(const PlanArgs& P, const Arrays& S, const uint32_t* s_q, uint32_t* s_flag) {
+__device__ int coop_wait(const PlanArgs& P, const Arrays& S, const uint32_t* s_q, uint32_t* s_flag, uint32_t sec) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   if (tid == 0) {
     coop_publish(P, s_q);
@@ -326,8 +326,12 @@ __device__ int coop_wait(const PlanArgs& P, const Arrays& S, const uint32_t* s_q
   __syncthreads();
   const uint32_t f = *s_flag;
   if (tid == 0) {
+    const unsigned long long dt = wall_clock64() - t0;
+    sec = min(sec, 7u);
     P.cc->waits += 1u;
-    P.cc->wait_ticks += wall_clock64() - t0;
+    P.cc->wait_ticks += dt;
+    P.cc->waits_sec[sec] += 1u;
+    P.cc->wait_sec[sec] += dt;
   }
   __syncthreads();
   return f == 3u ? COOP_GIVE_UP : (int)f;
@@ -354,10 +358,11 @@ __device__ void coop_requeue(const PlanArgs& P, const Arrays& S, uint32_t* s_q) 
 // Next hops are missing (refresh_codes returned nonzero and queued them). Coop mode: wait for the
 // workers and re-run the refresh until nothing is missing (true: continue in the kernel). Otherwise,
 // or if the workers do not answer, false: the caller exits for a host-side K3 pass.
-__device__ bool coop_resolve(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need, uint32_t* s_flag) {
+__device__ bool coop_resolve(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need, uint32_t* s_flag,
+                             uint32_t sec) {
   if (!P.coop) return false;
   for (int it = 0; it < 1024; ++it) {
-    const int st = coop_wait(P, S, s_q, s_flag);
+    const int st = coop_wait(P, S, s_q, s_flag, sec);
     if (st == COOP_GIVE_UP) return false;
     if (st == COOP_RETRY) coop_requeue(P, S, s_q);
     if (refresh_codes(P, S, s_q, s_need) == 0u) return true;
@@ -615,7 +620,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   if (s_ctl.section == SEC_RULES || s_ctl.section == SEC_MOVE) {
     // resuming after K3 resolved the missing next hops: every code starts dirty here
     const uint32_t q = refresh_codes(P, S, s_q, &s_need);
-    if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag)) {
+    if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
       if (tid == 0) {
         s_ctl.qcount = s_q[0];
         s_ctl.status = PLAN_NEED_QUERIES;
@@ -731,7 +736,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // the assignment exit's K3 batch (if any) already carries what the movement phase reads
       if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, s_q);
       if (P.coop && tid == 0) coop_publish(P, s_q);  // speculative pairs start resolving now
-      if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag)) {
+      if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
         if (tid == 0) {
           s_ctl.qcount = s_q[0];
           s_ctl.status = PLAN_NEED_QUERIES;
@@ -973,7 +978,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (s_miss) {
           // goals of the fired agents changed: their next hops (hence succ) must be looked up
           const uint32_t q = refresh_codes(P, S, s_q, &s_need);
-          if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag)) {
+          if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
             if (tid == 0) {
               s_ctl.qcount = s_q[0];
               s_ctl.status = PLAN_NEED_QUERIES;
@@ -1010,7 +1015,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       __syncthreads();
       if (s_ctl.miss) {
         const uint32_t q = refresh_codes(P, S, s_q, &s_need);
-        if (s_ctl.miss == 1 && q > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag)) {
+        if (s_ctl.miss == 1 && q > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
           if (tid == 0) s_ctl.miss = 0;
           __syncthreads();
           continue;  // resume the serial scan at ctl.i
@@ -1204,7 +1209,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       }
       if (s_miss) {
         // the missing codes are queued (pass 1 / pass 2) and their agents' codes are dirty
-        if (s_q[0] > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag)) continue;  // replay the open rounds
+        if (s_q[0] > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) continue;  // replay the open rounds
         if (tid == 0) {
           s_ctl.qcount = s_q[0];
           s_ctl.status = s_q[0] > 0 ? PLAN_NEED_QUERIES : PLAN_ERROR;
