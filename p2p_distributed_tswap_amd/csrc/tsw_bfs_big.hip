@@ -18,8 +18,7 @@
 //  * LDS: visited blocks V (nbp u64), two interleaved dedup-flag bitmaps, two block lists (u16).
 //  * HBM/L2 (read-only, shared by every workgroup, L2-resident): free-cell blocks FR, the per-block
 //    run-start numbering AB. Per-workgroup scratch (reused goal after goal): west-step blocks WL
-//    (nbp u64, plain read-modify-write by the block's owner thread of the level — a block appears
-//    once per level and levels are barrier-separated, so no atomics), compact run-start anchors
+//    (nbp u64, fire-and-forget workgroup-scope ORs, performed in L2), compact run-start anchors
 //    (nrs u16), list overflow (2 x nbp u16).
 //  * Level lvl processes exactly the blocks gaining cells at distance lvl:
 //    new = expand(V & parity(lvl-1)) & FR & ~V; a neighbour's concurrent update adds only
@@ -220,7 +219,9 @@ __global__ void __launch_bounds__(512) k_bfs_big(BigBfsArgs A) {
         if (act) {
           V[p] = vv;  // owner-exclusive within the level (the list is deduplicated)
           const uint64_t wln = nw & (((v0 << 1) & ~BCOL0) | ((vw >> 7) & BCOL0));
-          if (wln) WL[p] |= wln;
+          // fire-and-forget OR at workgroup scope (the scratch is this workgroup's; performed in
+          // L2, no load on the level's critical path)
+          if (wln) (void)__hip_atomic_fetch_or(WL + p, wln, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           bad |= nw == 0ull;  // a queued block must gain a cell
           anchors(p, nw, f0, fw, lvl);
         }

@@ -22,7 +22,7 @@
 //    flight per CU are bounded by LDS and the level loop is latency-bound, so the west-step
 //    blocks WL (bit set = the west neighbour was reached one level earlier; written once per
 //    activation, read only by the decode) live in per-wave global scratch, updated with
-//    fire-and-forget 64-bit atomic ORs.
+//    fire-and-forget 64-bit workgroup-scope atomic ORs (performed in L2).
 //  * Level lvl processes exactly the blocks that gain cells at distance lvl:
 //    new = expand(V & parity(lvl-1)) & FR & ~V (race-free inside the wave: the 4-grid is
 //    bipartite, so bits written during a level are never sources in the same level).
@@ -68,6 +68,16 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
 __device__ __forceinline__ uint32_t ld_nc16(const uint16_t* p) { return __builtin_nontemporal_load(p); }
 
 __device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
+
+// WL scratch belongs to one wave: a WORKGROUP-scope no-return OR is performed in this XCD's L2.
+// (Plain atomicOr is agent scope, which on a multi-XCD part bypasses the non-coherent L2 and runs
+// memory-side: every activation became HBM-side atomic traffic, ~1.5x the table bytes per goal.)
+__device__ __forceinline__ void wl_or(unsigned long long* p, unsigned long long v) {
+  (void)__hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wl_or32(unsigned int* p, unsigned int v) {
+  (void)__hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 __device__ __attribute__((noinline)) void blk_list_put_slow(uint16_t* Ln, uint16_t* On, uint32_t cap, uint32_t pos,
                                                            uint32_t entry) {
@@ -315,7 +325,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         // zero guard block
         V[p] = vv;
         const uint64_t wln = nw & (((v0 << 1) & ~COL0) | ((vw >> 7) & COL0));
-        if (wln) atomicOr(WL + p, (unsigned long long)wln);
+        if (wln) wl_or(WL + p, (unsigned long long)wln);
         bad |= act && nw == 0ull;  // entries must gain a cell
         anchors(p, nw, f0, fw, lvl);
         push(p, nw, vv, f0, fw, fe, fn, fs, vw, ve, vn, vs, Fn, Ln, On);
@@ -337,7 +347,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         const uint32_t vv = v0 | nw;
         V32[o] = vv;  // owner-exclusive (deduplicated list, one lane per half); idle lanes rewrite 0
         const uint32_t wln = nw & (((v0 << 1) & ~C0) | ((vw >> 7) & C0));
-        if (wln) atomicOr(WL32 + o, wln);
+        if (wln) wl_or32(WL32 + o, wln);
         const uint32_t nwp = partner(nw);
         bad |= act && (nw | nwp) == 0u;  // entries must gain a cell
         anchors2(p, nw, f0, fw, lvl);
