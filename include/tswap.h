@@ -168,6 +168,18 @@ int tsw_import_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k,
  * needs the exact A*). out: host buffer k*w*h. */
 int tsw_next_hop_tables(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint8_t *out);
 
+/* Goal-sharded K3: the fully resolved next-hop codes of k goals into
+ * caller-owned DEVICE memory (k*w*h bytes, row-major, codes as tsw_next_hop_tables). Builds the
+ * goals' tables if needed and resolves every multi-candidate cell with the exact A* (eager,
+ * whatever the context's next-hop policy): one rank's share of an all-gathered code table. */
+int tsw_next_hop_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint8_t *dev_out);
+
+/* Ingest k tables AND their next-hop codes (DEVICE memory: k*w*h u16 + k*w*h u8, e.g. the
+ * all-gather of tsw_dist_tables_device / tsw_next_hop_tables_device shards): steps then need
+ * neither K1 nor K3 for those goals. Code 0xFF (or a pending marker) = not resolved here. */
+int tsw_import_next_hops_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, const uint16_t *dev_dist,
+                                const uint8_t *dev_nh);
+
 /* Drop every goal table and next-hop code held by the context (device memory
  * is kept for reuse). Later calls rebuild what they need. */
 int tsw_clear_tables(tsw_ctx *ctx);

@@ -105,7 +105,8 @@ class Stats(ctypes.Structure):
 EXPORTED_SYMBOLS = (
     "tsw_create", "tsw_destroy", "tsw_last_error", "tsw_plan_mapd", "tsw_plan_mapd_trace",
     "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables", "tsw_dist_tables_device",
-    "tsw_import_tables_device", "tsw_next_hop_tables", "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing",
+    "tsw_import_tables_device", "tsw_next_hop_tables", "tsw_next_hop_tables_device", "tsw_import_next_hops_device",
+    "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing",
 )
 
 _lib = None
@@ -139,11 +140,14 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_import_tables_device.argtypes = [vp, P(u32), u32, vp]
     lib.tsw_clear_tables.argtypes = [vp]
     lib.tsw_next_hop_tables.argtypes = [vp, P(u32), u32, P(ctypes.c_uint8)]
+    lib.tsw_next_hop_tables_device.argtypes = [vp, P(u32), u32, vp]
+    lib.tsw_import_next_hops_device.argtypes = [vp, P(u32), u32, vp, vp]
     lib.tsw_get_stats.argtypes = [vp, P(Stats)]
     lib.tsw_reset_stats.argtypes = [vp]
     lib.tsw_set_timing.argtypes = [vp, ctypes.c_int]
     for name in ("tsw_plan_mapd", "tsw_plan_mapd_trace", "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables",
-                 "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_clear_tables", "tsw_next_hop_tables", "tsw_get_stats", "tsw_reset_stats",
+                 "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_clear_tables", "tsw_next_hop_tables",
+                 "tsw_next_hop_tables_device", "tsw_import_next_hops_device", "tsw_get_stats", "tsw_reset_stats",
                  "tsw_set_timing"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
@@ -318,6 +322,17 @@ class Planner:
         self._check(self._lib.tsw_next_hop_tables(self._ctx, _u32p(g), g.size,
                                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return out
+
+    def next_hop_tables_device(self, goals, dev_ptr: int):
+        """Resolved next-hop codes of `goals` (eager A*) into device memory (len(goals) x w*h u8)."""
+        g = np.ascontiguousarray(goals, dtype=np.uint32)
+        self._check(self._lib.tsw_next_hop_tables_device(self._ctx, _u32p(g), g.size, ctypes.c_void_p(dev_ptr)))
+
+    def import_next_hops_device(self, goals, dist_ptr: int, nh_ptr: int):
+        """Ingest tables + next-hop codes from device memory (e.g. an all-gather of rank shards)."""
+        g = np.ascontiguousarray(goals, dtype=np.uint32)
+        self._check(self._lib.tsw_import_next_hops_device(self._ctx, _u32p(g), g.size, ctypes.c_void_p(dist_ptr),
+                                                          ctypes.c_void_p(nh_ptr)))
 
     def clear_tables(self):
         self._check(self._lib.tsw_clear_tables(self._ctx))

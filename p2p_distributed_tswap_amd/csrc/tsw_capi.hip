@@ -1730,6 +1730,71 @@ int tsw_next_hop_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* 
   return TSW_OK;
 }
 
+int tsw_next_hop_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* dev_out) {
+  if (!c) return TSW_EINVAL;
+  if (k == 0) return TSW_OK;
+  if (!goals || !dev_out) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  std::vector<uint32_t> gv(goals, goals + k);
+  for (uint32_t g : gv)
+    if (!cell_id_ok(c, g)) RET(TSW_EINVAL, "goal cell off-grid or blocked");
+  HIPCHK(hipDeviceSynchronize());  // dev_out may come from another stream of the caller
+  TRY(ensure_tables(c, gv));
+  // eager resolution of this shard's multi-candidate cells, whatever the context's policy
+  std::vector<uint32_t> ug, us;
+  std::vector<uint8_t> seen(c->tab_count, 0);
+  for (uint32_t g : gv) {
+    const int32_t slot = c->h_goal_tab[g];
+    if (slot >= 0 && !seen[slot]) {
+      seen[slot] = 1;
+      ug.push_back(g);
+      us.push_back((uint32_t)slot);
+    }
+  }
+  TRY(resolve_all_unknown(c, ug, us));
+  const size_t ncell = c->G.ncell;
+  for (uint32_t i = 0; i < k; ++i) {
+    const int32_t slot = c->h_goal_tab[gv[i]];
+    HIPCHK(hipMemcpyAsync(dev_out + (size_t)i * ncell, c->d_nh + (size_t)slot * c->tstride, ncell,
+                          hipMemcpyDeviceToDevice, c->s));
+  }
+  HIPCHK(hipStreamSynchronize(c->s));
+  resolve_timing(c);
+  return TSW_OK;
+}
+
+int tsw_import_next_hops_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, const uint16_t* dev_dist,
+                                const uint8_t* dev_nh) {
+  if (!c) return TSW_EINVAL;
+  if (k == 0) return TSW_OK;
+  if (!goals || !dev_dist || !dev_nh) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  for (uint32_t i = 0; i < k; ++i)
+    if (!cell_id_ok(c, goals[i])) RET(TSW_EINVAL, "goal cell off-grid or blocked");
+  HIPCHK(hipDeviceSynchronize());  // produced on the caller's streams (e.g. an RCCL all-gather)
+  std::vector<uint32_t> newg, src, slots;
+  stamp_and_collect(c, goals, k, newg, &src);
+  if (newg.empty()) return TSW_OK;
+  auto ingest = [&]() -> int {
+    TRY(reserve_slots(c, newg.size(), slots));
+    const size_t ncell = c->G.ncell;
+    for (size_t j = 0; j < newg.size(); ++j) {
+      HIPCHK(hipMemcpyAsync(c->d_dist + (size_t)slots[j] * c->tstride, dev_dist + (size_t)src[j] * ncell,
+                            ncell * 2, hipMemcpyDeviceToDevice, c->s));
+      HIPCHK(hipMemcpyAsync(c->d_nh + (size_t)slots[j] * c->tstride, dev_nh + (size_t)src[j] * ncell, ncell,
+                            hipMemcpyDeviceToDevice, c->s));
+    }
+    // a pending marker from the producing context means "not resolved": unknown here (between
+    // calls no code of this store is pending, so one sweep over the whole store is exact)
+    HIPCHK(launch_reset_pending(c->d_nh, (uint64_t)c->tab_count * c->tstride, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    return TSW_OK;
+  };
+  TRY(finish_tables(c, ingest(), newg, slots));
+  resolve_timing(c);
+  return TSW_OK;
+}
+
 int tsw_clear_tables(tsw_ctx* c) {
   if (!c) return TSW_EINVAL;
   TRY(set_device(c));

@@ -1,0 +1,80 @@
+"""GPU: the multi-GPU ingest paths on one device ("the multi-GPU ingest path has never
+run on a GPU").
+
+* K1 shards built with tsw_dist_tables_device by two contexts ("ranks"), laid out rank-major as
+  sharding.build_and_allgather gathers them, then tsw_import_tables_device into a fresh context:
+  its plan equals the oracle's and the self-built plan, and the importing context ran no K1.
+* K3 shards (tsw_next_hop_tables_device: every multi-candidate cell resolved) + tables, imported
+  with tsw_import_next_hops_device: the plan needs neither K1 nor K3 for those goals and is exact.
+Device buffers come from the HIP runtime the library links (test_gpu_bfs._DevBuf)."""
+import numpy as np
+import pytest
+
+from p2p_distributed_tswap_amd import Planner, maps, sharding
+from oracle import OracleGraph
+from test_gpu_bfs import _DevBuf
+
+pytestmark = pytest.mark.gpu
+
+
+def _goalset(rows, starts, tasks):
+    w = len(rows[0])
+    cells = [y * w + x for x, y in starts.tolist()]
+    cells += [y * w + x for x, y in tasks[:, :2].tolist()] + [y * w + x for x, y in tasks[:, 2:].tolist()]
+    return np.array(sorted(set(cells)), dtype=np.uint32)
+
+
+def _gathered(rows, goals, world, codes):
+    """Build every rank's shard in its own context and lay the shards out as the all-gather does."""
+    ncell = len(rows) * len(rows[0])
+    per = sharding.shard_rows(goals.size, world)
+    dbuf = _DevBuf(world * per * ncell * 2)
+    cbuf = _DevBuf(world * per * ncell) if codes else None
+    for r, gl, off in sharding.gathered_blocks(goals, world):
+        with Planner(rows) as p:
+            p.dist_tables_device(gl, dbuf.ptr.value + off * ncell * 2)
+            if codes:
+                p.next_hop_tables_device(gl, cbuf.ptr.value + off * ncell)
+    return dbuf, cbuf, per
+
+
+@pytest.mark.parametrize("name,n,m,seed", [("warehouse", 150, 400, 9), ("rand32", 120, 300, 5)])
+def test_import_tables_then_plan(name, n, m, seed):
+    rows = maps.warehouse_map(170, 84, 0x170084) if name == "warehouse" else maps.random_map(32, 32, 0.2, 0x3232)
+    starts, tasks = maps.make_instance(rows, n, m, seed)
+    goals = _goalset(rows, starts, tasks)
+    ncell = len(rows) * len(rows[0])
+    dbuf, _, _ = _gathered(rows, goals, 2, codes=False)
+    ref, rgoal = OracleGraph(maps.rows_to_array(rows)).mapd(starts, tasks, 2000, trace_goals=True)
+    with Planner(rows) as p:
+        for _, gl, off in sharding.gathered_blocks(goals, 2):
+            p.import_tables_device(gl, dbuf.ptr.value + off * ncell * 2)
+        rec, goal = p.plan_mapd_arrays(starts, tasks, 2000, trace_goals=True)
+        assert p.stats()["bfs_goals"] == 0  # every table came from the import
+    with Planner(rows) as p:
+        rec2, _ = p.plan_mapd_arrays(starts, tasks, 2000)
+    assert np.array_equal(goal, rgoal) and np.array_equal(rec, ref)
+    assert np.array_equal(rec2, rec)
+
+
+@pytest.mark.parametrize("name,n,m,seed", [("rand32", 200, 600, 0x3232), ("rand16", 30, 90, 8)])
+def test_sharded_next_hops_then_plan(name, n, m, seed):
+    rows = maps.random_map(32, 32, 0.2, 0x3232) if name == "rand32" else maps.random_map(16, 16, 0.25, 3)
+    starts, tasks = maps.make_instance(rows, n, m, seed)
+    goals = _goalset(rows, starts, tasks)
+    ncell = len(rows) * len(rows[0])
+    og = OracleGraph(maps.rows_to_array(rows))
+    dbuf, cbuf, _ = _gathered(rows, goals, 2, codes=True)
+    codes = cbuf.to_host(np.empty((2 * sharding.shard_rows(goals.size, 2), ncell), dtype=np.uint8))
+    for _, gl, off in sharding.gathered_blocks(goals, 2):  # every gathered code == get_path()[1]
+        for j, g in enumerate(gl[:5]):
+            assert np.array_equal(codes[off + j], og.next_codes(int(g)))
+    ref, rgoal = og.mapd(starts, tasks, 2000, trace_goals=True)
+    with Planner(rows) as p:
+        for _, gl, off in sharding.gathered_blocks(goals, 2):
+            p.import_next_hops_device(gl, dbuf.ptr.value + off * ncell * 2, cbuf.ptr.value + off * ncell)
+        p.reset_stats()
+        rec, goal = p.plan_mapd_arrays(starts, tasks, 2000, trace_goals=True)
+        st = p.stats()
+    assert st["bfs_goals"] == 0 and st["astar_queries"] == 0  # no K1, no K3 on the planning GPU
+    assert np.array_equal(goal, rgoal) and np.array_equal(rec, ref)

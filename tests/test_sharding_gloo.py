@@ -51,6 +51,54 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _worker_codes(rank, world, port, q):
+    """K1 + K3 shards (oracle BFS tables and oracle next-hop codes = get_path(cell, goal)[1] for
+    every cell) all-gathered; every rank checks every gathered table and code table."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    from oracle import OracleGraph
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows = maps.random_map(14, 11, 0.2, 4)
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@")).astype(np.uint32)
+    goals = free[::5]
+
+    def build_dist(g, out):
+        out.copy_(torch.from_numpy(np.stack([og.bfs(int(x)) for x in g]).view(np.int16)))
+
+    def build_codes(g, out):
+        out.copy_(torch.from_numpy(np.stack([og.next_codes(int(x)) for x in g])))
+
+    full_d, full_c = sharding.build_and_allgather_codes(goals, cells.size, rank, world, build_dist, build_codes,
+                                                        dist, "cpu")
+    ok = True
+    for r, gl, off in sharding.gathered_blocks(goals, world):
+        for j, gg in enumerate(gl):
+            ok &= bool(np.array_equal(full_d[off + j].numpy().view(np.uint16), og.bfs(int(gg))))
+            ok &= bool(np.array_equal(full_c[off + j].numpy(), og.next_codes(int(gg))))
+    q.put((rank, ok, int(full_c.shape[0])))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_codes_allgather(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_codes, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_tables_allgather(world):
     ctx = mp.get_context("spawn")
