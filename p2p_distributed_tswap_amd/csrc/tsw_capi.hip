@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "tsw_internal.h"
@@ -169,8 +170,9 @@ struct tsw_ctx {
   AstarQuery* d_QT = nullptr;    // task chains of the current plan (host-filled)
   size_t qtcap = 0;
   uint32_t qt_count = 0;
-  uint32_t* h_started = nullptr; // pinned, coherent: set by the planner block when resident
-  uint32_t* d_started = nullptr;
+  uint32_t* h_flags = nullptr;   // pinned, coherent: [0] planner resident, [1] abort, [2] heartbeat
+  uint32_t* d_flags = nullptr;
+  uint64_t coop_aborts = 0;
 
   DevStatus* d_stat = nullptr;
   DevStatus* h_stat = nullptr;   // pinned, D2H
@@ -910,8 +912,8 @@ int ensure_coop(tsw_ctx* c, uint32_t n) {
   if (!c->d_cc) {
     HIPCHK(hipMalloc(&c->d_cc, sizeof(CoopCtl)));
     HIPCHK(hipHostMalloc(&c->h_cc, sizeof(CoopCtl), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(&c->h_started, 4, hipHostMallocCoherent | hipHostMallocMapped));
-    HIPCHK(hipHostGetDevicePointer((void**)&c->d_started, c->h_started, 0));
+    HIPCHK(hipHostMalloc(&c->h_flags, 16, hipHostMallocCoherent | hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void**)&c->d_flags, c->h_flags, 0));
     HIPCHK(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
   }
   if (!c->d_QS) {
@@ -984,7 +986,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
     P.QS = c->d_QS;
     P.qscap = (uint32_t)c->qscap;
     P.cc = c->d_cc;
-    P.started = c->d_started;
+    P.hflags = c->d_flags;
   }
   return P;
 }
@@ -1024,6 +1026,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     // task chains take half the workers at most (a quarter with many agents: their needed bursts
     // are larger), the rest stay free for the pairs the planner waits on
     W.tmask = P.n > 2000u ? 3u : 1u;
+    W.hflags = c->d_flags;
     W.gs_all = c->d_gs;
     W.epochs = c->d_epochs;
     W.heaps = c->d_heaps;
@@ -1037,7 +1040,10 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       HIPCHK(hipMemsetAsync(c->d_cc, 0, sizeof(CoopCtl), c->s));
       const uint32_t nt = P.mode == MODE_MAPD ? c->qt_count : 0u;
       if (nt) HIPCHK(hipMemcpyAsync(&c->d_cc->head_t, &c->qt_count, 4, hipMemcpyHostToDevice, c->s));
-      *(volatile uint32_t*)c->h_started = 0u;
+      volatile uint32_t* hf = c->h_flags;
+      hf[0] = 0u;
+      hf[1] = 0u;
+      hf[2] = 0u;
     }
     {
       Timer t(c, CAT_WALK);
@@ -1049,13 +1055,37 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       // first thing), so they can never take the CU it needs; if the flag is late they start anyway
       // and the planner falls back to exits (no deadlock either way)
       const auto t0 = std::chrono::steady_clock::now();
-      while (!*(volatile uint32_t*)c->h_started &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500)) {
+      while (!c->h_flags[0] && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500)) {
       }
       HIPCHK(launch_astar_workers(W, wcfg, c->s2));
       c->st.astar_launches++;
     }
     HIPCHK(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(PlanCtl), hipMemcpyDeviceToHost, c->s));
+    if (coop) {
+      // watchdog: the planner publishes its timestep count; if it stops moving for 10 s while the
+      // planner still runs, raise `abort`: its waits give up (it exits to the host) and the workers
+      // leave, and the rest of this call runs in exit mode. A protocol fault can then cost time but
+      // never hang the call.
+      volatile uint32_t* hf = c->h_flags;
+      uint32_t last = hf[2];
+      auto seen = std::chrono::steady_clock::now();
+      for (;;) {
+        const hipError_t q = hipStreamQuery(c->s);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) HIPCHK(q);
+        const uint32_t hb = hf[2];
+        const auto now = std::chrono::steady_clock::now();
+        if (hb != last) {
+          last = hb;
+          seen = now;
+        } else if (!hf[1] && now - seen > std::chrono::seconds(10)) {
+          hf[1] = 1u;
+          ++c->coop_aborts;
+          fprintf(stderr, "[tswap] coop watchdog: planner made no step for 10 s; falling back to exit mode\n");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
     HIPCHK(hipStreamSynchronize(c->s));
     if (coop) {
       HIPCHK(hipStreamSynchronize(c->s2));
@@ -1104,6 +1134,17 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     c->st.plan_exits[std::min<uint32_t>(k.section, 7u)]++;
     if (coop) {
       if (k.status != PLAN_NEED_QUERIES) RET(TSW_EINVAL, "plan kernel stopped without resolvable next hops");
+      if (c->h_flags[1]) {
+        // watchdog fired: finish this call in exit mode (host-side K3 passes at planner exits);
+        // pairs the aborted workers left queued are unqueued first
+        HIPCHK(launch_reset_pending(c->d_nh, (uint64_t)c->tab_count * c->tstride, c->s));
+        HIPCHK(hipStreamSynchronize(c->s));
+        P.coop = 0;
+        PlanCtl resume = k;
+        resume.status = PLAN_RUNNING;
+        resume.qcount = 0;
+        return run_plan_impl(c, P, resume);
+      }
       continue;  // the workers resolved every needed pair before exiting: relaunch
     }
     if (k.status != PLAN_NEED_QUERIES || k.qcount == 0 || k.qcount > P.qcap)
@@ -1391,7 +1432,7 @@ void tsw_destroy(tsw_ctx* c) {
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
   fre(c->d_cc); fre(c->d_QS); fre(c->d_QT);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
-  if (c->h_started) (void)hipHostFree(c->h_started);
+  if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->s2) (void)hipStreamDestroy(c->s2);
   if (c->h_stat) hipHostFree(c->h_stat);
   if (c->h_ctl) hipHostFree(c->h_ctl);

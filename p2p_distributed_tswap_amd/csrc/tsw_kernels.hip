@@ -1223,9 +1223,12 @@ __device__ __forceinline__ bool w_cas(uint32_t* p, uint32_t expect, uint32_t wan
 // lane 0: claim the next pair (0: needed queue, 1: speculative queue, 2: task chain, -1: exit).
 // Task chains (long, lowest priority) only go to workers with take_t: the others stay free for the
 // pairs the planner needs or will need soon.
-__device__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t) {
+__device__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags) {
   const unsigned long long t0 = wall_clock64();
   for (uint32_t spin = 0;; ++spin) {
+    if ((spin & 63u) == 63u && hflags &&
+        __hip_atomic_load(&hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+      return -1;  // host watchdog abort
     const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
     if (cn < hn) {
       if (w_cas(&cc->claim_n, cn, cn + 1u)) {
@@ -1350,7 +1353,7 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
   for (;;) {
     int which = -1;
     uint32_t idx = 0;
-    if (lane == 0) which = worker_claim(A.cc, &idx, take_t);
+    if (lane == 0) which = worker_claim(A.cc, &idx, take_t, A.hflags);
     which = __builtin_amdgcn_readfirstlane(which);
     if (which < 0) break;
     idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);

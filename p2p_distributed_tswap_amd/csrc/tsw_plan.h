@@ -82,7 +82,9 @@ struct PlanArgs {
   AstarQuery* QS;
   uint32_t qscap;
   CoopCtl* cc;
-  uint32_t* started;              // host-visible: set when the planner block is resident
+  // host-visible (pinned, system-coherent) words: [0] set when the planner block is resident,
+  // [1] abort (host watchdog: planner waits give up, workers exit), [2] planner heartbeat (timesteps)
+  uint32_t* hflags;
 };
 
 // flinks: the pointer-doubling buffers F1/F2 alone in LDS (when the agent arrays are not)
@@ -106,6 +108,7 @@ struct WorkerArgs {
   uint32_t gs_lds;    // 0: u32 g-scores in the global slots, 1: u32 in LDS, 2: bytes in LDS
   uint32_t stage_fb;  // free-cell bitmap staged in LDS (else read from global memory / L2)
   uint32_t tmask;     // workers with (blockIdx & tmask) == tmask also take task-chain jobs
+  const uint32_t* hflags;  // host watchdog words (hflags[1] = abort)
   uint32_t* gs_all;   // per-wave global g-score slots (tier 2 / tier 3), ncell u32 each
   uint32_t* epochs;   // per-slot tag epochs
   uint64_t* heaps;    // per-wave global heaps (tier 3), ghcap entries each

@@ -310,7 +310,8 @@ __device__ int coop_wait(const PlanArgs& P, const Arrays& S, const uint32_t* s_q
       if (c == NH_UNKNOWN) break;
       const unsigned long long dt = wall_clock64() - t0;
       if (dt > COOP_GIVE_UP_TICKS || ld_agent(&P.cc->err) != 0u ||
-          (dt > COOP_NO_WORKER_TICKS && ld_agent(&P.cc->alive) == 0u)) {
+          (dt > COOP_NO_WORKER_TICKS && ld_agent(&P.cc->alive) == 0u) ||
+          (P.hflags && __hip_atomic_load(&P.hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
         st = COOP_GIVE_UP;
         break;
       }
@@ -614,7 +615,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_tsec = 7;  // entry / copy-in
     // coop mode: tell the host the planner is resident, so the workers it launches next cannot
     // take the CUs this block needs
-    if (P.started) __hip_atomic_store(P.started, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (P.hflags) __hip_atomic_store(&P.hflags[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
   if (s_ctl.section == SEC_RULES || s_ctl.section == SEC_MOVE) {
@@ -1254,6 +1255,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       if (tid == 0) {
         s_ctl.t = t + 1;
         s_ctl.steps_run += 1;
+        if (P.hflags) __hip_atomic_store(&P.hflags[2], s_ctl.steps_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((s_ctl.unused == 0u && !busy) || s_ctl.t > s_ctl.max_t) {
           s_ctl.status = PLAN_DONE;
           s_ctl.section = SEC_DONE;

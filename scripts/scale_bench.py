@@ -38,9 +38,9 @@ INSTANCES = {
 
 
 def _heartbeat(stop, t0):
-    """A long plan is one blocking C call: print progress so a batch runner sees it is alive."""
-    while not stop.wait(30.0):
-        print(f"[scale_bench] still planning, {time.perf_counter() - t0:.0f} s", flush=True)
+    """A long plan is one blocking C call: print progress (stderr) so a batch runner sees it is alive."""
+    while not stop.wait(20.0):
+        print(f"[scale_bench] still planning, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
 
 
 def main():
@@ -60,20 +60,22 @@ def main():
         rows, starts, tasks = fac()
         n, m = starts.shape[0], tasks.shape[0]
         h, w = len(rows), len(rows[0])
-        with Planner(rows) as p:
-            p.plan_mapd_arrays(starts[:8], tasks[:8], 4)  # context warm-up (not timed)
-            p.clear_tables()
-            p.reset_stats()
-            t0 = time.perf_counter()
-            stop = threading.Event()
-            hb = threading.Thread(target=_heartbeat, args=(stop, t0), daemon=True)
-            hb.start()
-            try:
+        stop = threading.Event()
+        hb = threading.Thread(target=_heartbeat, args=(stop, time.perf_counter()), daemon=True)
+        hb.start()
+        try:
+            with Planner(rows) as p:
+                print(f"[scale_bench] {name}: warm-up", file=sys.stderr, flush=True)
+                p.plan_mapd_arrays(starts[:8], tasks[:8], 4)  # context warm-up (not timed)
+                p.clear_tables()
+                p.reset_stats()
+                print(f"[scale_bench] {name}: plan", file=sys.stderr, flush=True)
+                t0 = time.perf_counter()
                 rec, _ = p.plan_mapd_arrays(starts, tasks, args.max_t)
-            finally:
-                stop.set()
-            gpu_s = time.perf_counter() - t0
-            st = p.stats()
+                gpu_s = time.perf_counter() - t0
+                st = p.stats()
+        finally:
+            stop.set()
         T = rec.shape[1]
         og = OracleGraph(maps.rows_to_array(rows))
         tc = time.perf_counter()
