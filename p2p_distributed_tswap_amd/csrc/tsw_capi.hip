@@ -912,8 +912,6 @@ int ensure_coop(tsw_ctx* c, uint32_t n) {
   if (!c->d_cc) {
     HIPCHK(hipMalloc(&c->d_cc, sizeof(CoopCtl)));
     HIPCHK(hipHostMalloc(&c->h_cc, sizeof(CoopCtl), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc(&c->h_flags, 16, hipHostMallocCoherent | hipHostMallocMapped));
-    HIPCHK(hipHostGetDevicePointer((void**)&c->d_flags, c->h_flags, 0));
     HIPCHK(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
   }
   if (!c->d_QS) {
@@ -982,11 +980,11 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.tasks_lds = tk;
   // coop mode: lazy next hops only (eager tables have nothing left to resolve)
   P.coop = (c->tun.coop && P.prefetch && c->d_cc && c->d_QS) ? 1u : 0u;
+  P.hflags = c->d_flags;  // watchdog words, both modes
   if (P.coop) {
     P.QS = c->d_QS;
     P.qscap = (uint32_t)c->qscap;
     P.cc = c->d_cc;
-    P.hflags = c->d_flags;
   }
   return P;
 }
@@ -1040,6 +1038,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       HIPCHK(hipMemsetAsync(c->d_cc, 0, sizeof(CoopCtl), c->s));
       const uint32_t nt = P.mode == MODE_MAPD ? c->qt_count : 0u;
       if (nt) HIPCHK(hipMemcpyAsync(&c->d_cc->head_t, &c->qt_count, 4, hipMemcpyHostToDevice, c->s));
+    }
+    {
       volatile uint32_t* hf = c->h_flags;
       hf[0] = 0u;
       hf[1] = 0u;
@@ -1061,11 +1061,12 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       c->st.astar_launches++;
     }
     HIPCHK(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(PlanCtl), hipMemcpyDeviceToHost, c->s));
-    if (coop) {
+    {
       // watchdog: the planner publishes its timestep count; if it stops moving for 10 s while the
-      // planner still runs, raise `abort`: its waits give up (it exits to the host) and the workers
-      // leave, and the rest of this call runs in exit mode. A protocol fault can then cost time but
-      // never hang the call.
+      // planner still runs, raise `abort`. In coop mode its waits give up (it exits to the host),
+      // the workers leave and the rest of the call runs in exit mode; a planner stuck anywhere else
+      // sees the flag in its round loops and exits with ERR_ABORT and its position. A fault can
+      // then cost time or fail the call, but never hang it.
       volatile uint32_t* hf = c->h_flags;
       uint32_t last = hf[2];
       auto seen = std::chrono::steady_clock::now();
@@ -1106,6 +1107,13 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       }
     }
     const PlanCtl& k = *c->h_ctl;
+    if (k.err & ERR_ABORT) {
+      char buf[256];
+      snprintf(buf, sizeof buf,
+               "planner stopped by the watchdog (no timestep for 10 s): t %u section %u cursor %u, %u rule rounds, "
+               "%u move rounds", k.t, k.section, k.i, k.rule_rounds, k.move_rounds);
+      RET(TSW_EINVAL, buf);
+    }
     if (k.err) {
       char buf[128];
       snprintf(buf, sizeof buf, "plan kernel error bits 0x%x", k.err);
@@ -1407,6 +1415,10 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if (c->wall_khz <= 0) c->wall_khz = 100000;
   if ((e = hipHostMalloc(&c->h_ctl, sizeof(PlanCtl), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned ctl", e);
+  if ((e = hipHostMalloc(&c->h_flags, 16, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
+    return fail("pinned flags", e);
+  if ((e = hipHostGetDevicePointer((void**)&c->d_flags, c->h_flags, 0)) != hipSuccess)
+    return fail("flags device pointer", e);
   memset(c->h_stat, 0, sizeof(DevStatus));
   size_t freeb = 0, totalb = 0;
   hipMemGetInfo(&freeb, &totalb);

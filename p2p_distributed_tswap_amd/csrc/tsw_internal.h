@@ -86,5 +86,6 @@ constexpr uint32_t ERR_NO_TABLE = 8u;
 constexpr uint32_t ERR_WALK_OVERFLOW = 16u;
 constexpr uint32_t ERR_BFS_LIST = 32u;     // k_bfs_wave: a queued word gained no cell (logic error)
 constexpr uint32_t ERR_DECIDE_LIST = 64u;  // k_decide: a nearby list longer than DEC_MAX_LIST
+constexpr uint32_t ERR_ABORT = 128u;       // k_plan: stopped by the host watchdog (no step for 10 s)
 
 }  // namespace tsw

@@ -266,6 +266,11 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// host watchdog (coop and exit mode): the planner polls this in every loop that can run long
+__device__ __forceinline__ bool plan_abort(const PlanArgs& P) {
+  return P.hflags && __hip_atomic_load(&P.hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
+
 // thread 0: make every entry queued so far visible to the workers (caller: after a barrier)
 __device__ __forceinline__ void coop_publish(const PlanArgs& P, const uint32_t* s_q) {
   const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap);
@@ -526,7 +531,7 @@ template <bool AG, bool OC>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[2], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag;
+  __shared__ uint32_t s_q[2], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[16], s_tlast, s_tp;
@@ -608,6 +613,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_ctl = *P.ctl;
     s_ctl.status = PLAN_RUNNING;
     s_exit = 0;
+    s_abort = 0;
     s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     s_q[1] = 0;  // speculative queue (coop mode)
     for (int k = 0; k < 16; ++k) s_tick[k] = 0;
@@ -633,8 +639,18 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
 
   for (;;) {
     if (s_exit) break;
+    if (s_abort) {  // watchdog: exit with the position recorded in ctl (section, cursor, rounds)
+      if (tid == 0) {
+        s_ctl.status = PLAN_ERROR;
+        P.ctl->err |= ERR_ABORT;
+        s_exit = 1;
+      }
+      __syncthreads();
+      break;
+    }
     const uint32_t sec = s_ctl.section;
     if (tid == 0) {
+      if (plan_abort(P)) s_abort = 1;
       const unsigned long long now = wall_clock64();
       s_tick[s_tsec] += now - s_tlast;
       s_tlast = now;
@@ -889,7 +905,15 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             uint32_t sk = SUCC_TERM;
             bool f = false, onck = false;
             uint64_t m = 0;
-            for (;;) {
+            for (uint32_t spin = 1;; ++spin) {
+              if ((spin & 1023u) == 0u &&
+                  (uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? (plan_abort(P) ? 1u : 0u) : 0u)) {
+                if (lane == 0) {
+                  s_abort = 1;
+                  s_best = NO_AGENT;
+                }
+                break;
+              }
               if (!loaded) {
                 if (base >= n) {
                   if (lane == 0) {
@@ -976,6 +1000,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         __syncthreads();
         PLAN_TICK(14);
         if (s_best == NO_AGENT) break;
+        if (tid == 0 && (s_ctl.rule_rounds & 1023u) == 1023u && plan_abort(P)) s_abort = 1;
         if (s_miss) {
           // goals of the fired agents changed: their next hops (hence succ) must be looked up
           const uint32_t q = refresh_codes(P, S, s_q, &s_need);
@@ -998,6 +1023,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           PLAN_TICK(15);
         }
       }
+      if (s_abort) continue;  // watchdog: exit at the top of the section loop, position kept
       if (s_exit) break;
       if (tid == 0) {
         s_ctl.section = SEC_PRE2;
@@ -1142,8 +1168,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           s_best = NO_AGENT;
           s_ctl.move_rounds += 1;
           if (P.dbg) s_tp = wall_clock64();
+          if ((s_ctl.move_rounds & 1023u) == 0u && plan_abort(P)) s_abort = 1;
         }
         __syncthreads();
+        if (s_abort) break;
         tag = (uint64_t)s_ctl.move_rounds << 32;
         int open = 0;
         for (uint32_t k = tid; k < n; k += bd) open |= pass1(k) ? 1 : 0;
@@ -1189,7 +1217,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                 s_miss = 0;
                 s_best = NO_AGENT;
                 s_ctl.move_rounds += 1;
+                if ((s_ctl.move_rounds & 1023u) == 0u && plan_abort(P)) s_abort = 1;
               }
+              __threadfence_block();
+              if (*(volatile uint32_t*)&s_abort) break;
               __threadfence_block();
               tag = (uint64_t)(*(volatile uint32_t*)&s_ctl.move_rounds) << 32;
               const bool op = kk != NO_AGENT && pass1(kk);
@@ -1208,6 +1239,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         }
         __syncthreads();
       }
+      if (s_abort) continue;  // watchdog: exit at the top of the section loop, position kept
       if (s_miss) {
         // the missing codes are queued (pass 1 / pass 2) and their agents' codes are dirty
         if (s_q[0] > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) continue;  // replay the open rounds
