@@ -212,6 +212,8 @@ typedef struct {
     double coop_wait_ms;
     double coop_wait_sec_ms[8]; /* ... by planner section (plan_section_ms indices) */
     uint64_t coop_waits_sec[8];
+    /* rules-phase cycle relabels: block-wide pointer doubling / incremental walks */
+    uint64_t relabels_full, relabels_inc;
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

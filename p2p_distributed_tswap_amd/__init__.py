@@ -90,6 +90,7 @@ class Stats(ctypes.Structure):
         ("plan_exits", ctypes.c_uint64 * 8), ("table_evictions", ctypes.c_uint64),
         ("coop_waits", ctypes.c_uint64), ("coop_wait_ms", ctypes.c_double),
         ("coop_wait_sec_ms", ctypes.c_double * 8), ("coop_waits_sec", ctypes.c_uint64 * 8),
+        ("relabels_full", ctypes.c_uint64), ("relabels_inc", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -1119,6 +1119,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       snprintf(buf, sizeof buf, "plan kernel error bits 0x%x", k.err);
       RET((k.err & ERR_NO_TABLE) ? TSW_EINVAL : TSW_EOVERFLOW, buf);
     }
+    c->st.relabels_full += k.relabel_full;
+    c->st.relabels_inc += k.relabel_inc;
     if (k.status == PLAN_DONE) {
       c->chase_id = k.chase_id;
       c->st.rule_rounds += k.rule_rounds;

@@ -38,6 +38,8 @@ struct PlanCtl {
   uint32_t steps_run;
   uint32_t rule_rounds;  // first-firing rounds executed (rules phase)
   uint32_t move_rounds;  // decidability rounds executed (movement phase)
+  uint32_t relabel_full;  // rules-phase relabels by block-wide pointer doubling
+  uint32_t relabel_inc;   // ... and incremental ones (walks from the changed agents)
 };
 
 struct PlanArgs {

@@ -167,6 +167,51 @@ __device__ void rules_init(const PlanArgs& P, const Arrays& S) {
   __syncthreads();
 }
 
+// Incremental rules relabel (thread 0) after a firing changed the goals of the `cnt` agents in
+// `lst` (rule-4 rotation: every member of the rotated cycle; rule-3 swap: b and s) and the refresh
+// re-looked-up their next hops. In the rules phase nobody moves (OCC is fixed), so only these
+// agents' successors changed: SUCC / CANDC are recomputed for them alone, and a cycle that appears
+// must pass through one of them while a cycle that disappears contained one (all of a rotated
+// cycle's members are in `lst`, and rule 3 only extends the chain of s, which was terminal). So
+// each changed agent's cycle label is a walk along SUCC from it: back to itself = on a cycle (label
+// the cycle), TERM / a self-loop / an agent on another cycle = not. Walks average ~2 hops on the
+// warehouse grids, against a block-wide pointer doubling over every agent. Returns false (caller
+// relabels in full) if a walk runs past `limit` hops.
+__device__ bool rules_relabel_changed(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt,
+                                      uint32_t limit) {
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint32_t k = lst[i];
+    const uint32_t s = succ_of(P, S, k);
+    S.SUCC[k] = s;
+    S.ONC[k] = 0;
+    uint8_t cc = NHC_DIRTY;
+    if (s != SUCC_TERM && s != k && S.V[s] == S.G[s] && S.GT[k] >= 0)
+      cc = P.nh[(uint64_t)S.GT[k] * P.nstride + S.V[s]];
+    S.CANDC[k] = cc;
+  }
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint32_t a = lst[i];
+    if (S.ONC[a]) continue;  // labelled by an earlier walk of this loop
+    uint32_t x = S.SUCC[a];
+    uint32_t steps = 0;
+    while (x != SUCC_TERM && x != a) {
+      if (S.ONC[x]) break;  // joins a cycle that does not contain a
+      const uint32_t nx = S.SUCC[x];
+      if (nx == x) break;    // self-loop (stay code): a chain end
+      x = nx;
+      if (++steps > limit) return false;
+    }
+    if (x == a) {
+      uint32_t y = a;
+      do {
+        S.ONC[y] = 1;
+        y = S.SUCC[y];
+      } while (y != a);
+    }
+  }
+  return true;
+}
+
 __device__ __forceinline__ void put_query(const PlanArgs& P, uint8_t* p, uint32_t qi, uint32_t v, uint32_t g,
                                           int32_t tab) {
   *p = NH_PENDING;  // only once the slot is ours: a pending code is always really queued
@@ -777,6 +822,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // candidate k, so a swap needs no global round trip on the serial path.
       if (P.dbg && tid == 0) s_tp = wall_clock64();
       rules_init(P, S);
+      if (tid == 0) s_ctl.relabel_full += 1;
       if (P.prefetch) rules_prefetch(P, S, s_q);
       if (P.coop && tid == 0) coop_publish(P, s_q);
       if (tid == 0) s_cnt = 0;
@@ -1013,7 +1059,24 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             __syncthreads();
             break;
           }
-          rules_init(P, S);
+          // only the agents in `list` changed since the last labelling: relabel incrementally when
+          // they are few (a rotation's members), else by pointer doubling over every agent
+          if (s_cnt != NO_AGENT && s_cnt <= 64u) {
+            if (tid == 0) {
+              const bool ok = rules_relabel_changed(P, S, list, s_cnt, 4096u);
+              s_flag = ok ? 1u : 0u;
+              if (ok) s_ctl.relabel_inc += 1;
+            }
+            __syncthreads();
+            if (!s_flag) {
+              rules_init(P, S);
+              if (tid == 0) s_ctl.relabel_full += 1;
+            }
+          } else {
+            rules_init(P, S);
+            if (tid == 0) s_ctl.relabel_full += 1;
+          }
+          __syncthreads();
           if (P.prefetch) {
             if (P.wide_prefetch && s_cnt != NO_AGENT) rules_prefetch_list(P, S, s_q, list, s_cnt);
             else rules_prefetch(P, S, s_q);

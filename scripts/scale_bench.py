@@ -99,7 +99,8 @@ def main():
             "plan_exits_by_section": st["plan_exits"], "rule_rounds": st["rule_rounds"],
             "coop_waits": st["coop_waits"], "coop_wait_ms": round(st["coop_wait_ms"], 2),
             "coop_wait_sec_ms": [round(x, 2) for x in st["coop_wait_sec_ms"]],
-            "coop_waits_sec": st["coop_waits_sec"], "env": {k: v for k, v in os.environ.items() if k.startswith("TSW_")},
+            "coop_waits_sec": st["coop_waits_sec"], "relabels_full": st["relabels_full"],
+            "relabels_inc": st["relabels_inc"], "env": {k: v for k, v in os.environ.items() if k.startswith("TSW_")},
         }
         print(json.dumps(out), flush=True)
 
