@@ -195,7 +195,21 @@ __device__ bool rules_relabel_changed(const PlanArgs& P, const Arrays& S, const 
     uint32_t x = S.SUCC[a];
     uint32_t steps = 0;
     while (x != SUCC_TERM && x != a) {
-      if (S.ONC[x]) break;  // joins a cycle that does not contain a
+      if (S.ONC[x]) {
+        // x is labelled: a cycle that still stands (every member of a cycle that broke is in
+        // `lst` and was cleared above). It may contain a itself — `lst` accumulates every agent
+        // changed since the last labelling, including members of a cycle a rule-3 swap closed
+        // and labelled in fire() — so go once around it: meeting a puts a on it, back at x
+        // without a means a only drains into it. A walk that does neither means a stale label:
+        // relabel in full.
+        uint32_t y = S.SUCC[x];
+        while (y != x && y != a) {
+          if (y == SUCC_TERM || S.SUCC[y] == y || ++steps > limit) return false;
+          y = S.SUCC[y];
+        }
+        x = y;  // == a: on the cycle (labelled below); == x: not
+        break;
+      }
       const uint32_t nx = S.SUCC[x];
       if (nx == x) break;    // self-loop (stay code): a chain end
       x = nx;
