@@ -66,6 +66,7 @@ struct Tunables {
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
   bool task_chains = true;        // TSW_TASK_CHAINS=0: no task-chain jobs for the coop workers
+  int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
 
   static Tunables from_env() {
     Tunables t;
@@ -93,6 +94,7 @@ struct Tunables {
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
     t.task_chains = num("TSW_TASK_CHAINS", 0, 1, 1) != 0;
+    t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
     return t;
   }
 };
@@ -940,7 +942,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.candc = c->d_candc;
   P.f1 = c->d_f1;
   P.f2 = c->d_f2;
-  P.ap = c->d_ap;
+  P.mk = c->d_ap;
   P.occ = c->d_occ;
   P.mu = c->d_mu;
   P.has_dups = *c->h_dups;
@@ -1029,7 +1031,10 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.epochs = c->d_epochs;
     W.heaps = c->d_heaps;
     W.ghcap = c->hcap;
-    wcfg = worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap);
+    wcfg = worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs);
+    if (c->tun.plan_debug)
+      fprintf(stderr, "[k_plan] workers: %u waves, g-scores %u, heap %u entries, %zu B LDS\n", wcfg.waves, wcfg.gs_lds,
+              wcfg.hcap, wcfg.lds);
     wcfg.waves = std::min(wcfg.waves, c->nslots);
   }
   for (uint64_t round = 0;; ++round) {
@@ -1125,12 +1130,25 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       c->chase_id = k.chase_id;
       c->st.rule_rounds += k.rule_rounds;
       if (c->tun.plan_debug) {
-        unsigned long long tk[16];
+        unsigned long long tk[24];
         HIPCHK(hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[k_plan] wave rules kcycles: load %.0f stale %.0f fast %.0f update %.0f slow %.0f rot %.0f | "
+                "loads %llu fast firings %llu\n", tk[16] / 1e3, tk[17] / 1e3, tk[18] / 1e3, tk[19] / 1e3, tk[20] / 1e3,
+                tk[21] / 1e3, tk[22], tk[23]);
         fprintf(stderr, "[k_plan] steps %u rule rounds %u move rounds %u launches %llu | move A-E us %.0f %.0f %.0f %.0f %.0f"
                 " | rules scan %.0f fire %.0f relabel %.0f\n", k.steps_run, k.rule_rounds, k.move_rounds,
                 (unsigned long long)round + 1ull, tk[8] / 100.0, tk[9] / 100.0, tk[10] / 100.0, tk[11] / 100.0,
                 tk[12] / 100.0, tk[13] / 100.0, tk[14] / 100.0, tk[15] / 100.0);
+        if (coop) {
+          const CoopCtl& cc = *c->h_cc;
+          fprintf(stderr, "[k_plan] needed pairs unresolved (never queued / queued speculatively): PRE1 %u/%u RULES %u/%u "
+                  "MOVE %u/%u | fast rule-3 firings %u (code from global memory %u) | chain queries %llu of %llu\n", cc.dbg_need[0], cc.dbg_need[1], cc.dbg_need[2],
+                  cc.dbg_need[3], cc.dbg_need[4], cc.dbg_need[5], cc.dbg_need[6], cc.dbg_need[7],
+                  (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
+          fprintf(stderr, "[k_plan] worker A* ms (queries): needed %.1f (%u) spec %.1f (%u) task chains %.1f (%u)\n",
+                  cc.wbusy[0] / (double)c->wall_khz, cc.wcount[0], cc.wbusy[1] / (double)c->wall_khz, cc.wcount[1],
+                  cc.wbusy[2] / (double)c->wall_khz, cc.wcount[2]);
+        }
       }
       // exit mode: pairs the prefetch queued but no firing needed — resolve them so no table entry
       // is left PENDING for later calls (coop mode: the workers drained the needed queue)
@@ -1410,8 +1428,8 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned status", e);
   if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
-  if ((e = hipMalloc(&c->d_ticks, 16 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
-  if ((e = hipMemsetAsync(c->d_ticks, 0, 16 * sizeof(unsigned long long), c->s)) != hipSuccess)
+  if ((e = hipMalloc(&c->d_ticks, 24 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
+  if ((e = hipMemsetAsync(c->d_ticks, 0, 24 * sizeof(unsigned long long), c->s)) != hipSuccess)
     return fail("memset ticks", e);
   hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, c->device);
   if (c->wall_khz <= 0) c->wall_khz = 100000;
@@ -1885,7 +1903,7 @@ int tsw_reset_stats(tsw_ctx* c) {
   const uint64_t tabs = c->st.tables;
   c->st = tsw_stats{};
   c->st.tables = tabs;
-  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 16 * sizeof(unsigned long long), c->s);
+  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 24 * sizeof(unsigned long long), c->s);
   return TSW_OK;
 }
 

@@ -68,6 +68,12 @@ struct CoopCtl {
   unsigned long long chain_queries;  // ... of which on task chains
   unsigned long long wait_sec[8];    // wait ticks by planner section (SEC_*)
   uint32_t waits_sec[8];             // waits by planner section
+  // diagnostics (TSW_PLAN_DEBUG): pairs a step needed that were unresolved, per section group
+  // (PRE1, RULES, MOVE, other) x (never queued, queued speculatively but not resolved yet)
+  uint32_t dbg_need[8];
+  // diagnostics: worker wall-clock ticks inside A* and queries, by queue (needed, spec, chain)
+  unsigned long long wbusy[4];
+  uint32_t wcount[4];
   uint32_t pad4[2];
 };
 

@@ -1304,7 +1304,7 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
   if (lane == 0) __hip_atomic_fetch_add(&A.cc->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // exact A* for (v, goal): tier 1 LDS heap + LDS (or global) g-scores, tier 2 global u32
   // g-scores, tier 3 global heap (the k_astar_wave -> k_astar hand-off chain, in one wave)
-  auto resolve = [&](uint32_t v, uint32_t goal) -> uint8_t {
+  auto resolve_exact = [&](uint32_t v, uint32_t goal) -> uint8_t {
     int32_t L = 0;
     uint8_t code = NH_UNKNOWN;
     if (gs_lds == 2u) {
@@ -1335,6 +1335,16 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
     }
     return code;
   };
+  uint32_t cur_q = 0;  // diagnostics: queue of the query being resolved (0 needed, 1 spec, 2 chain)
+  auto resolve = [&](uint32_t v, uint32_t goal) -> uint8_t {
+    const unsigned long long tr0 = wall_clock64();
+    const uint8_t code = resolve_exact(v, goal);
+    if (lane == 0) {
+      __hip_atomic_fetch_add(&A.cc->wbusy[cur_q], wall_clock64() - tr0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&A.cc->wcount[cur_q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return code;
+  };
   // the code (or NH_UNKNOWN after a global-heap overflow, flagged in cc->err): an agent-scope
   // store the planner's polling load sees
   auto publish_code = [&](uint32_t v, int32_t tab, uint8_t code, bool chain) {
@@ -1362,6 +1372,7 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
     const uint32_t* e = reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : A.QT) + idx);
     const uint32_t v = w_ld(e), goal = w_ld(e + 1);
     const int32_t tab = (int32_t)w_ld(e + 2);
+    cur_q = (uint32_t)which;
     if (which < 2) {
       publish_code(v, tab, resolve(v, goal), false);
       continue;
@@ -1387,7 +1398,7 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
   if (lane == 0) A.epochs[blockIdx.x] = ep;
 }
 
-WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want) {
+WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs) {
   const size_t fbb = (size_t)G.H * G.Ww * 4u;
   const uint32_t want = hcap_want ? std::min(hcap_want, WAVE_HCAP) : WAVE_HCAP;
   auto make = [&](uint32_t m, bool fb) {
@@ -1403,6 +1414,12 @@ WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_
     return c;
   };
   const uint32_t m = wave_gs_mode(G);
+  const bool fits = force_gs == 0 || (force_gs == 1 && G.ncell <= WAVE_GS_LDS_MAX) ||
+                    (force_gs == 2 && G.ncell <= WAVE_GB_LDS_MAX);
+  if (force_gs >= 0 && fits) {  // A/B: another g-score placement than the default
+    WorkerCfg f = make((uint32_t)force_gs, true);
+    if (f.hcap >= 64u) return f;
+  }
   WorkerCfg c = make(m, true);
   // grids whose byte g-scores fit LDS (<= 120k cells): with many agents, trade the LDS g-scores for
   // 3x the waves (global u32 slots, L2-resident at this size)

@@ -61,7 +61,7 @@ struct PlanArgs {
   uint8_t* candc; // per agent rule-3 next-hop prefetch (global copy)
   uint32_t* f1;   // pointer-doubling buffers, n + 1 entries each (global copy)
   uint32_t* f2;
-  uint32_t* ap;   // rule-4 cycle members
+  uint32_t* mk;   // per agent batch marks of the wave rules rounds (global copy, n + 1 entries)
   uint32_t* occ;  // per cell occupancy
   uint64_t* mu;   // per cell round-tagged lowest undecided targeting agent (global copy)
   const uint32_t* pick_xy;
@@ -123,7 +123,7 @@ struct WorkerCfg {
   uint32_t gs_lds, stage_fb, hcap, waves;
   size_t lds;
 };
-WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want);
+WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs = -1);
 hipError_t launch_astar_workers(const WorkerArgs& A, const WorkerCfg& cfg, hipStream_t s);
 
 }  // namespace tsw

@@ -66,6 +66,10 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
   return x;
 }
 
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {  // set bits of m below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -85,7 +89,9 @@ struct Arrays {
   uint8_t* NHC;    // next-hop code of (V, G) or NHC_DIRTY
   uint8_t* DEC;    // movement-round state
   uint8_t* ONC;    // rules: agent lies on a cycle of succ
-  uint8_t* CANDC;  // rules: next hop of succ(k)'s cell toward k's goal (rule-3 prefetch)
+  uint8_t* CANDC;  // rules: next hop of succ(k)'s cell toward k's goal — what succ(k) needs when it takes
+                   // k's goal (rule-3 swap, or the rotation of a cycle through both)
+  uint32_t* MK;    // rules (wave rounds): lowest batch lane touching each agent, ~0 when clear
   uint32_t* F1;    // rules: pointer-doubling buffers (n + 1 entries, n = terminal sink)
   uint32_t* F2;
   uint32_t* OCC;   // per cell: lowest agent | OCC_FLAG, or OCC_NONE
@@ -142,7 +148,7 @@ __device__ void rules_init(const PlanArgs& P, const Arrays& S) {
     S.F1[k] = s == SUCC_TERM ? n : s;
     S.ONC[k] = 0;
     uint8_t cc = NHC_DIRTY;
-    if (s != SUCC_TERM && s != k && S.V[s] == S.G[s] && S.GT[k] >= 0)
+    if (s != SUCC_TERM && s != k && S.GT[k] >= 0)
       cc = P.nh[(uint64_t)S.GT[k] * P.nstride + S.V[s]];
     S.CANDC[k] = cc;
   }
@@ -185,7 +191,7 @@ __device__ bool rules_relabel_changed(const PlanArgs& P, const Arrays& S, const 
     S.SUCC[k] = s;
     S.ONC[k] = 0;
     uint8_t cc = NHC_DIRTY;
-    if (s != SUCC_TERM && s != k && S.V[s] == S.G[s] && S.GT[k] >= 0)
+    if (s != SUCC_TERM && s != k && S.GT[k] >= 0)
       cc = P.nh[(uint64_t)S.GT[k] * P.nstride + S.V[s]];
     S.CANDC[k] = cc;
   }
@@ -290,7 +296,8 @@ __device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uin
 // appended to the launch's K3 queue (s_q counts every pair queued since the launch began,
 // speculative prefetches included). Returns how many dirty agents still lack a code
 // (block-uniform): the planner must exit for K3 iff that is nonzero.
-__device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need) {
+__device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need,
+                                  uint32_t sec) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   if (tid == 0) *s_need = 0;
   __syncthreads();
@@ -307,6 +314,10 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
     if (code <= NH_STAY) {
       S.NHC[k] = code;
     } else {
+      if (P.dbg && P.coop && (code == NH_UNKNOWN || code == NH_PENDING_S)) {
+        const uint32_t grp = sec == SEC_PRE1 ? 0u : sec == SEC_RULES ? 1u : sec == SEC_MOVE ? 2u : 3u;
+        atomicAdd(&P.cc->dbg_need[2u * grp + (code == NH_PENDING_S ? 1u : 0u)], 1u);
+      }
       enqueue_pair(P, v, g, tab, s_q);  // no-op if already queued (PENDING)
       atomicAdd(s_need, 1u);
     }
@@ -321,6 +332,9 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
 // agent-scope loads and write each code with an agent-scope store, which the planner polls with
 // agent-scope loads. A code, once written, never changes, so a stale plain read of the table can
 // only see an older state (UNKNOWN / PENDING) — a conservative "unresolved", never a wrong hop.
+// (Write-through entries and PENDING marks with relaxed head stores instead were measured slower:
+// every write-through drops the line from this XCD's L2, and the planner's next plain loads of
+// those table lines missed — movement passes 3x slower.)
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -392,7 +406,12 @@ __device__ int coop_wait(const PlanArgs& P, const Arrays& S, const uint32_t* s_q
   const uint32_t f = *s_flag;
   if (tid == 0) {
     const unsigned long long dt = wall_clock64() - t0;
-    sec = min(sec, 7u);
+    // diagnostics: PRE1 waits classed by what the step's ASSIGN did (5: assigned a task, 6: only
+    // pickup arrivals, 7: neither — walking agents)
+    {
+      const uint32_t kslot[6] = {0u, 0u, 3u, 5u, 6u, 7u};
+      sec = (P.dbg && (sec >> 8)) ? kslot[sec >> 8] : min(sec & 0xFFu, 7u);
+    }
     P.cc->waits += 1u;
     P.cc->wait_ticks += dt;
     P.cc->waits_sec[sec] += 1u;
@@ -430,7 +449,7 @@ __device__ bool coop_resolve(const PlanArgs& P, const Arrays& S, uint32_t* s_q, 
     const int st = coop_wait(P, S, s_q, s_flag, sec);
     if (st == COOP_GIVE_UP) return false;
     if (st == COOP_RETRY) coop_requeue(P, S, s_q);
-    if (refresh_codes(P, S, s_q, s_need) == 0u) return true;
+    if (refresh_codes(P, S, s_q, s_need, sec & 0xFFu) == 0u) return true;
   }
   return false;
 }
@@ -469,24 +488,25 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
 // rules_prefetch restricted to the agents a firing changed (rule 3: b and s, rule 4: the cycle):
 // only their goals, hence their next hops and successors, moved, so only their pairs are new.
 // After rules_init (SUCC valid).
+__device__ __forceinline__ void prefetch_changed(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t k) {
+  if (spec_full(P, s_q)) return;
+  const int32_t tab = S.GT[k];
+  if (tab < 0) return;
+  const uint8_t c = S.NHC[k];
+  if (c < NH_STAY && S.V[k] != S.G[k]) {
+    const uint32_t u = step_cell(S.V[k], c, P.W);
+    if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) prefetch_pair(P, u, S.G[k], tab, s_q);
+  }
+  const uint32_t s = S.SUCC[k];
+  if (s == SUCC_TERM || s == k) return;
+  const uint32_t vs = S.V[s];
+  if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) prefetch_pair(P, vs, S.G[k], tab, s_q);
+}
+
 __device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t* s_q, const uint32_t* lst,
                                     uint32_t cnt) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
-  for (uint32_t i = tid; i < cnt; i += bd) {
-    if (spec_full(P, s_q)) break;
-    const uint32_t k = lst[i];
-    const int32_t tab = S.GT[k];
-    if (tab < 0) continue;
-    const uint8_t c = S.NHC[k];
-    if (c < NH_STAY && S.V[k] != S.G[k]) {
-      const uint32_t u = step_cell(S.V[k], c, P.W);
-      if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) prefetch_pair(P, u, S.G[k], tab, s_q);
-    }
-    const uint32_t s = S.SUCC[k];
-    if (s == SUCC_TERM || s == k) continue;
-    const uint32_t vs = S.V[s];
-    if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) prefetch_pair(P, vs, S.G[k], tab, s_q);
-  }
+  for (uint32_t i = tid; i < cnt; i += bd) prefetch_changed(P, S, s_q, lst[i]);
   __syncthreads();
 }
 
@@ -593,8 +613,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   __shared__ uint32_t s_q[2], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
-  __shared__ unsigned long long s_tick[16], s_tlast, s_tp;
+  __shared__ unsigned long long s_tick[24], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
+  __shared__ uint32_t s_nassign, s_npick;  // diagnostics: this step's assignments / pickup arrivals
   const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6, nwaves = bd >> 6;
   const uint32_t n = P.n, W = P.W;
 
@@ -614,6 +635,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     S.SUCC = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
     S.F1 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
     S.F2 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
+    S.MK = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
     S.NHC = carve(n);
     S.DEC = carve(n);
     S.ONC = carve(n);
@@ -634,6 +656,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     S.DEC = P.dec;
     S.ONC = P.onc;
     S.CANDC = P.candc;
+    S.MK = P.mk;  // (batched firing runs only with the agent arrays in LDS; this copy stays unused)
   }
   if constexpr (OC) {
     S.OCC = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
@@ -654,6 +677,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     S.PXY = P.pick_xy;
     S.USED = P.used;
   }
+  for (uint32_t k = tid; k <= n; k += bd) S.MK[k] = 0xFFFFFFFFu;
   for (uint32_t k = tid; k < n; k += bd) {
     const uint32_t g = P.g[k];
     if constexpr (AG) {
@@ -675,7 +699,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_abort = 0;
     s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     s_q[1] = 0;  // speculative queue (coop mode)
-    for (int k = 0; k < 16; ++k) s_tick[k] = 0;
+    for (int k = 0; k < 24; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
     // coop mode: tell the host the planner is resident, so the workers it launches next cannot
@@ -685,7 +709,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   __syncthreads();
   if (s_ctl.section == SEC_RULES || s_ctl.section == SEC_MOVE) {
     // resuming after K3 resolved the missing next hops: every code starts dirty here
-    const uint32_t q = refresh_codes(P, S, s_q, &s_need);
+    const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
     if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
       if (tid == 0) {
         s_ctl.qcount = s_q[0];
@@ -717,6 +741,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     }
     if (sec == SEC_ASSIGN) {
       // ---- K4: state machine + task assignment (tswap.rs:106-139) -------------
+      if (tid == 0) s_nassign = s_npick = 0;
       for (uint32_t base = 0; base < n; base += bd) {
         const uint32_t i = base + tid;
         bool needy = false;
@@ -748,6 +773,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             if (v == S.G[ai]) {
               if (st == ST_TO_PICKUP) {
                 st = ST_TO_DELIVERY;
+                ++s_npick;
                 const int32_t tk = P.task[ai];
                 if (tk >= 0) {
                   const uint32_t ng = P.dlv[tk];
@@ -791,6 +817,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                 s_ctl.unused -= 1u;
                 P.task[ai] = (int32_t)t;
                 P.st[ai] = ST_TO_PICKUP;
+                ++s_nassign;
                 const uint32_t ng = P.pick[t];
                 S.G[ai] = ng;
                 S.GT[ai] = P.goal_tab[ng];
@@ -807,12 +834,15 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       }
       __syncthreads();
     } else if (sec == SEC_PRE1 || sec == SEC_PRE2) {
-      const uint32_t q = refresh_codes(P, S, s_q, &s_need);
+      const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
       // step start: queue every agent's next hop from the cell it is about to enter now, so
       // the assignment exit's K3 batch (if any) already carries what the movement phase reads
       if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, s_q);
       if (P.coop && tid == 0) coop_publish(P, s_q);  // speculative pairs start resolving now
-      if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
+      // diagnostics: PRE1 waits by timestep bucket (t < 50, < 150, < 400, < 1000, later)
+      const uint32_t tt = s_ctl.t;
+      const uint32_t wkind = sec == SEC_PRE1 ? (tt < 50 ? 1u : tt < 150 ? 2u : tt < 400 ? 3u : tt < 1000 ? 4u : 5u) : 0u;
+      if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section | (wkind << 8))) {
         if (tid == 0) {
           s_ctl.qcount = s_q[0];
           s_ctl.status = PLAN_NEED_QUERIES;
@@ -858,7 +888,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         uint32_t s, ns, flags;
         bool fs, b_at, s_at;
       };
-      constexpr uint32_t FO_MISS = 1u, FO_RESCAN = 2u;
+      // FO_ROT: a rule-4 rotation of o.ns members (listed in S.F2) whose next hops are dirty
+      constexpr uint32_t FO_MISS = 1u, FO_RESCAN = 2u, FO_ROT = 4u;
       auto fire = [&](uint32_t b) -> FireOut {
         FireOut o;
         o.flags = 0;
@@ -878,6 +909,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           S.G[s] = gb;
           S.GT[s] = tb;
           S.CANDC[s] = NHC_DIRTY;
+          S.CANDC[b] = NHC_DIRTY;  // b's goal changed (a later rotation through b must not use it)
           o.b_at = vb == gs;
           o.s_at = vs == gb;
           if (o.b_at) {  // shared start cell: b now at its goal
@@ -898,7 +930,16 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
               // new cycle through s?
               uint32_t x = ns;
               uint32_t it = 0;
-              for (; it < n && x != SUCC_TERM && x != s; ++it) x = S.SUCC[x];
+              // a labelled agent lies on a standing cycle, which cannot contain s (terminal until
+              // now), and a self-loop is a chain end: neither leads back to s
+              for (; it < n && x != SUCC_TERM && x != s; ++it) {
+                const uint32_t nx = S.SUCC[x];
+                if (S.ONC[x] || nx == x) {
+                  x = SUCC_TERM;
+                  break;
+                }
+                x = nx;
+              }
               if (P.dbg) s_tick[9] += it;  // diagnostics: rule-3 cycle-walk hops
               if (x == s) {
                 uint32_t y = s;
@@ -936,8 +977,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           S.G[b] = last_goal;
           S.GT[b] = last_tab;
           S.NHC[b] = NHC_DIRTY;
-          s_miss = 1;  // members' next hops changed: refresh + full relabel below
-          o.flags |= FO_MISS;
+          // members' next hops changed: the wave rounds settle them in place (rot_settle), the
+          // block rounds refresh + relabel below
+          o.flags |= FO_ROT;
+          o.ns = L;
           for (uint32_t kk = 0; kk < L; ++kk) note_changed(ap[kk]);
           if (P.dbg) s_tick[11] += 1;  // diagnostics: rule-4 rotations
         }
@@ -949,22 +992,101 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // 64 agents from the cursor, the fire is lane 0 of the same wave, so a round needs no
       // workgroup barrier and no cross-wave reduction; the block joins only when a firing
       // changed next hops (refresh + relabel) or the phase ends.
+      // Wave 0, after a rotation of L members (S.F2): every member's next hop for its new goal
+      // (lanes in parallel, from CANDC of its predecessor when current), then an incremental
+      // relabel from the members (lane 0; the labels were exact before the rotation and only the
+      // members' successors changed). False (block path: refresh, wait, relabel) if a code is
+      // unresolved or a walk runs long.
+      auto rot_settle = [&](uint32_t L) -> bool {
+        const uint32_t* ap = S.F2;
+        bool bad = false;
+        for (uint32_t i = lane; i < L; i += 64u) {
+          const uint32_t a = ap[i];
+          if (S.V[a] == S.G[a]) continue;
+          // a took the goal of its predecessor pa on the cycle and sits at succ(pa)'s cell: the code
+          // is CANDC[pa] when that is still current, else a table read
+          const uint32_t pa = ap[i == 0u ? L - 1u : i - 1u];
+          uint8_t code = S.CANDC[pa];
+          if (code > NH_STAY) {
+            const int32_t tab = S.GT[a];
+            code = tab >= 0 ? P.nh[(uint64_t)tab * P.nstride + S.V[a]] : NH_UNKNOWN;
+          }
+          if (code <= NH_STAY) S.NHC[a] = code;
+          else bad = true;
+        }
+        if (__ballot(bad)) return false;
+        __threadfence_block();
+        uint32_t ok = 0;
+        if (lane == 0) ok = rules_relabel_changed(P, S, ap, L, 4096u) ? 1u : 0u;
+        if (!__builtin_amdgcn_readfirstlane(ok)) return false;
+        if (lane == 0) s_ctl.relabel_inc += 1;
+        __threadfence_block();
+        // (no prefetch here: the members' next hops are set, and the next step's walk-ahead
+        // prefetch covers their paths; a publish costs an L2 write-back)
+        return true;
+      };
       const bool wave_scan = n <= P.wave_rules_max;
       for (;;) {
         if (wave_scan) {
           if (wid == 0) {
             // Per-lane state of the chunk [base, base+64): successor sk, ONC bit, firing flag f.
             // A rule-3 swap (b, s) changes the firing predicate of other agents only through
-            // s's successor and the at-goal status of b and s, which fire() returns in
-            // registers: the flags are updated in place and the next firing agent is the
-            // next set bit of the ballot — no LDS re-scan and no cursor round trip per round.
-            // The firing lane itself applies the swap (its b, s are already in registers).
+            // s's successor and the at-goal status of b and s: the flags are updated in place
+            // and the next firing agent is the next set bit of the ballot — no LDS re-scan and
+            // no cursor round trip per round.
+            // Each candidate lane also precomputes its own swap (s's cell / goal / slot, the code of
+            // s's new next hop, s's new successor ns and whether ns sits at its goal), all lanes at
+            // once, so the common firing — a rule-3 swap whose code is resolved — is a handful of
+            // stores by the firing lane with nothing to wait for. A firing invalidates the
+            // precomputation of every lane it touches (k, its successor or its ns among b, s);
+            // stale lanes redo it when one of them is next. Anything else (rule 4, a missing code,
+            // a shared start cell) takes fire().
             __threadfence_block();
             uint32_t base = *(volatile uint32_t*)&s_ctl.i;
+            uint32_t nc = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_cnt);  // changed-list length
+            uint32_t rr = 0;                                                          // fast firings
             bool loaded = false;
             uint32_t sk = SUCC_TERM;
             bool f = false, onck = false;
             uint64_t m = 0;
+            bool pv = false;  // precomputed swap valid
+            uint32_t p_vs = 0, p_gs = 0, p_gk = 0, p_ns = SUCC_TERM;
+            int32_t p_ts = -1, p_tk = -1;
+            uint32_t p_code = NH_UNKNOWN;
+            bool p_fsv = false, p_walk = false;
+            auto precompute = [&](bool want) {
+              if (!want) return;
+              const uint32_t k = base + lane;
+              p_vs = S.V[sk];
+              p_gs = S.G[sk];
+              p_ts = S.GT[sk];
+              p_gk = S.G[k];
+              p_tk = S.GT[k];
+              const uint32_t vk = S.V[k];
+              uint32_t code = S.CANDC[k];
+              bool ok = p_vs == p_gs && vk != p_gs;  // rule 3 without a shared start cell
+              if (ok && code > NH_STAY) code = p_tk >= 0 ? P.nh[(uint64_t)p_tk * P.nstride + p_vs] : NH_UNKNOWN;
+              ok = ok && code <= NH_STAY;
+              p_code = code;
+              uint32_t ns = SUCC_TERM;
+              if (ok && p_vs != p_gk) {
+                const uint32_t oc = S.OCC[step_cell(p_vs, code, W)];
+                ns = oc == OCC_NONE ? SUCC_TERM : (oc & OCC_IDX);
+              }
+              p_ns = ns;
+              p_fsv = ok && ns != SUCC_TERM && ns != sk && S.V[ns] == S.G[ns];
+              p_walk = ok && ns != SUCC_TERM && ns != sk && !p_fsv;  // s's new successor moves: cycle check
+              pv = ok;
+            };
+            // diagnostics (TSW_PLAN_DEBUG): shader cycles per part of the loop -> s_tick[16..23]
+            unsigned long long pt = P.dbg ? clock64() : 0ull;
+            auto prof = [&](int slot) {
+              if (P.dbg) {
+                const unsigned long long nw = clock64();
+                if (lane == 0) s_tick[slot] += nw - pt;
+                pt = nw;
+              }
+            };
             for (uint32_t spin = 1;; ++spin) {
               if ((spin & 1023u) == 0u &&
                   (uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? (plan_abort(P) ? 1u : 0u) : 0u)) {
@@ -986,13 +1108,17 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                 f = false;
                 onck = false;
                 sk = SUCC_TERM;
+                pv = false;
                 if (k < n) {
                   sk = S.SUCC[k];
                   onck = S.ONC[k] != 0;
                   f = sk != SUCC_TERM && sk != k && (S.V[sk] == S.G[sk] || onck);
                 }
                 m = __ballot(f);
+                precompute(f);
                 loaded = true;
+                if (P.dbg && lane == 0) s_tick[22] += 1;
+                prof(16);
               }
               if (!m) {
                 base += 64u;
@@ -1001,19 +1127,173 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
               }
               const uint32_t l = (uint32_t)__builtin_ctzll(m);
               const uint32_t b = base + l;
+              // the next firing lane's precomputation is stale: redo it for every stale candidate
+              if (!__builtin_amdgcn_readlane((int)(pv ? 1u : 0u), (int)l)) precompute(f && !pv);
+              prof(17);
+              if (AG && __builtin_amdgcn_readlane((int)(pv && !p_walk ? 1u : 0u), (int)l)) {
+                // ---- batch (agent arrays in LDS): the longest run of firing lanes from l whose rule-3 swaps cannot see each
+                // other. Firing lanes mark the agents their swap writes (b = k, s = sk) with their lane
+                // (LDS min). A lane whose own agent, successor or precomputed ns carries an earlier
+                // lane's mark reads state that earlier swap changes; the batch ends before the first
+                // such lane (firing or not: a non-firing s may start firing) and before the first firing
+                // lane that is not a plain precomputed swap. The swaps of the batch then touch disjoint
+                // agents and read nothing another one writes, so applying them at once equals applying
+                // them in agent order (tswap.rs:180-252). Lanes past the batch that it touched reload.
+                const uint32_t k = base + lane;
+                const bool fire_l = ((m >> lane) & 1ull) != 0ull;  // m holds lanes >= l only
+                const bool simple = fire_l && pv && !p_walk;
+                if (simple) {
+                  atomicMin(&S.MK[k], lane);
+                  atomicMin(&S.MK[sk], lane);
+                }
+                __threadfence_block();
+                uint32_t c = 0xFFFFFFFFu;
+                if (k < n) {
+                  c = S.MK[k];
+                  if (sk != SUCC_TERM) c = min(c, S.MK[sk]);
+                  if (pv && p_ns != SUCC_TERM) c = min(c, S.MK[p_ns]);
+                }
+                const uint64_t bm = __ballot(lane >= l && (c < lane || (fire_l && !simple)));
+                const uint32_t cut = bm ? (uint32_t)__builtin_ctzll(bm) : 64u;
+                const uint64_t batch = cut >= 64u ? m : (m & ((1ull << cut) - 1ull));
+                const bool inb = ((batch >> lane) & 1ull) != 0ull;
+                if (inb) {  // rule 3 (tswap.rs:198-202): b <-> s goals, s's new code and successor
+                  S.G[k] = p_gs;
+                  S.GT[k] = p_ts;
+                  S.G[sk] = p_gk;
+                  S.GT[sk] = p_tk;
+                  S.CANDC[sk] = NHC_DIRTY;
+                  S.CANDC[k] = NHC_DIRTY;
+                  S.NHC[sk] = (uint8_t)p_code;
+                  S.SUCC[sk] = p_ns;
+                }
+                const bool touched = lane >= cut && c < cut;
+                __threadfence_block();
+                if (simple) {
+                  S.MK[k] = 0xFFFFFFFFu;
+                  S.MK[sk] = 0xFFFFFFFFu;
+                }
+                __threadfence_block();
+                if (touched && k < n) {  // exact state after the batch, from LDS
+                  sk = S.SUCC[k];
+                  onck = S.ONC[k] != 0;
+                  f = sk != SUCC_TERM && sk != k && (S.V[sk] == S.G[sk] || onck);
+                  pv = false;
+                }
+                // b and s of every swap join the changed list (targeted prefetch at the next relabel)
+                const uint32_t nb = (uint32_t)__popcll(batch);
+                if (nc != NO_AGENT && nc + 2u * nb <= LIST_CAP) {
+                  if (inb) {
+                    const uint32_t r = lane_rank(batch);
+                    list[nc + 2u * r] = k;
+                    list[nc + 2u * r + 1u] = sk;
+                  }
+                  nc += 2u * nb;
+                } else {
+                  nc = NO_AGENT;
+                }
+                rr += nb;
+                const uint32_t last = 63u - (uint32_t)__builtin_clzll(batch);
+                if (lane == last) {
+                  s_best = k;
+                  s_miss = 0;
+                  s_ctl.i = k + 1u;
+                }
+                m = last == 63u ? 0ull : (__ballot(f) & ~((2ull << last) - 1ull));
+                if (P.dbg && lane == 0) s_tick[23] += nb;
+                prof(18);
+                continue;
+              }
               uint32_t r_fl = 0, r_s = 0, r_ns = 0, r_bits = 0;
-              if (lane == l) {
-                s_best = b;
-                s_miss = 0;
-                const FireOut r = fire(b);
-                r_fl = r.flags;
-                r_s = r.s;
-                r_ns = r.ns;
-                r_bits = (r.fs ? 1u : 0u) | (r.b_at ? 2u : 0u) | (r.s_at ? 4u : 0u);
+              const bool fast = __builtin_amdgcn_readlane((int)(pv ? 1u : 0u), (int)l) != 0;
+              if (fast) {
+                // rule 3 (tswap.rs:198-202) from registers: b <-> s goals, s's new code and successor
+                if (lane == l) {
+                  const uint32_t s = sk;
+                  S.G[b] = p_gs;
+                  S.GT[b] = p_ts;
+                  S.G[s] = p_gk;
+                  S.GT[s] = p_tk;
+                  S.CANDC[s] = NHC_DIRTY;
+                  S.CANDC[b] = NHC_DIRTY;
+                  S.NHC[s] = (uint8_t)p_code;
+                  S.SUCC[s] = p_ns;
+                  s_best = b;
+                  s_miss = 0;
+                  s_ctl.i = b + 1;
+                  bool fs = p_fsv;
+                  if (p_ns != SUCC_TERM && p_ns != s && !p_fsv) {
+                    // new cycle through s? (as in fire(): a labelled agent or a self-loop ends it)
+                    uint32_t x = p_ns;
+                    uint32_t it = 0;
+                    for (; it < n && x != SUCC_TERM && x != s; ++it) {
+                      const uint32_t nx = S.SUCC[x];
+                      if (S.ONC[x] || nx == x) {
+                        x = SUCC_TERM;
+                        break;
+                      }
+                      x = nx;
+                    }
+                    if (P.dbg) s_tick[9] += it;
+                    if (x == s) {
+                      uint32_t y = s;
+                      do {
+                        S.ONC[y] = 1;
+                        y = S.SUCC[y];
+                      } while (y != s);
+                      r_fl = FO_RESCAN;
+                    }
+                    fs = false;
+                  }
+                  r_s = s;
+                  r_ns = p_ns;
+                  r_bits = (fs ? 1u : 0u) | (p_vs == p_gk ? 4u : 0u);
+                }
+                // b and s joined the changed list (targeted prefetch at the phase end / next relabel)
+                const uint32_t fsx = (uint32_t)__builtin_amdgcn_readlane((int)r_s, (int)l);
+                if (nc != NO_AGENT && nc + 2u <= LIST_CAP) {
+                  if (lane == 0) {
+                    list[nc] = b;
+                    list[nc + 1u] = fsx;
+                  }
+                  nc += 2u;
+                } else {
+                  nc = NO_AGENT;
+                }
+                ++rr;
+                prof(18);
+              } else {
+                if (lane == 0) s_cnt = nc;
+                __threadfence_block();
+                if (lane == l) {
+                  s_best = b;
+                  s_miss = 0;
+                  const FireOut r = fire(b);
+                  r_fl = r.flags;
+                  r_s = r.s;
+                  r_ns = r.ns;
+                  r_bits = (r.fs ? 1u : 0u) | (r.b_at ? 2u : 0u) | (r.s_at ? 4u : 0u);
+                }
+                __threadfence_block();
+                nc = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_cnt);
+                prof(20);
               }
               __threadfence_block();
               const uint32_t fl = (uint32_t)__builtin_amdgcn_readlane((int)r_fl, (int)l);
               if (fl & FO_MISS) break;
+              if (fl & FO_ROT) {
+                // settle the rotation inside the wave when every member's new next hop is already
+                // resolved (the rules prefetch queued them): rescan from b + 1 without a block join
+                const bool settled = rot_settle((uint32_t)__builtin_amdgcn_readlane((int)r_ns, (int)l));
+                prof(21);
+                if (settled) {
+                  base = b + 1u;
+                  loaded = false;
+                  continue;
+                }
+                if (lane == 0) s_miss = 1;
+                break;
+              }
               if (fl & FO_RESCAN) {
                 base = b + 1u;
                 loaded = false;
@@ -1023,6 +1303,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
               const uint32_t fns = (uint32_t)__builtin_amdgcn_readlane((int)r_ns, (int)l);
               const uint32_t fbits = (uint32_t)__builtin_amdgcn_readlane((int)r_bits, (int)l);
               const uint32_t k = base + lane;
+              // precomputations that read b or s (own goal, successor's cell/goal, ns's goal) are stale
+              if (k == b || k == fs_ || sk == b || sk == fs_ || p_ns == b || p_ns == fs_) pv = false;
               if (k == fs_) {
                 sk = fns;
                 f = (fbits & 1u) != 0;
@@ -1031,6 +1313,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                 else if (sk == b) f = (fbits & 2u) != 0 || onck;
               }
               m = __ballot(f) & ~((2ull << l) - 1ull);  // l == 63: shift wraps to 0, mask 0
+              prof(19);
+            }
+            if (lane == 0) {
+              s_cnt = nc;
+              s_ctl.rule_rounds += rr;
             }
           }
         } else {
@@ -1053,8 +1340,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
             for (uint32_t w = 0; w < nwaves; ++w) b = s_wcount[w] < b ? s_wcount[w] : b;
             s_best = b;
             s_miss = 0;
-            if (b != NO_AGENT) fire(b);
-            else s_ctl.i = n;
+            if (b != NO_AGENT) {
+              if (fire(b).flags & FO_ROT) s_miss = 1;
+            } else {
+              s_ctl.i = n;
+            }
           }
         }
         __syncthreads();
@@ -1063,7 +1353,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         if (tid == 0 && (s_ctl.rule_rounds & 1023u) == 1023u && plan_abort(P)) s_abort = 1;
         if (s_miss) {
           // goals of the fired agents changed: their next hops (hence succ) must be looked up
-          const uint32_t q = refresh_codes(P, S, s_q, &s_need);
+          const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
           if (q > 0 && !coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
             if (tid == 0) {
               s_ctl.qcount = s_q[0];
@@ -1118,7 +1408,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       }
       __syncthreads();
       if (s_ctl.miss) {
-        const uint32_t q = refresh_codes(P, S, s_q, &s_need);
+        const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
         if (s_ctl.miss == 1 && q > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
           if (tid == 0) s_ctl.miss = 0;
           __syncthreads();
@@ -1400,7 +1690,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     P.ctl->err |= err;
     s_tick[s_tsec] += wall_clock64() - s_tlast;
     if (P.sec_ticks)
-      for (int k = 0; k < 16; ++k) P.sec_ticks[k] += s_tick[k];
+      for (int k = 0; k < 24; ++k) P.sec_ticks[k] += s_tick[k];
   }
 }
 
@@ -1430,7 +1720,7 @@ __global__ void k_occ_flag(uint32_t* occ, const uint32_t* cnt, uint32_t ncell, u
 size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks, bool flinks) {
   auto r16 = [](size_t b) { return (b + 15u) & ~(size_t)15u; };
   size_t b = r16(1024 * 4);
-  if (agents) b += 4 * r16((size_t)n * 4) + 2 * r16((size_t)(n + 1) * 4) + 4 * r16(n);
+  if (agents) b += 4 * r16((size_t)n * 4) + 3 * r16((size_t)(n + 1) * 4) + 4 * r16(n);
   else if (flinks) b += 2 * r16((size_t)(n + 1) * 4);
   if (occ) b += r16((size_t)ncell * 4) + r16((size_t)ncell * 8);
   if (tasks) b += r16((size_t)m * 4) + r16(m);
