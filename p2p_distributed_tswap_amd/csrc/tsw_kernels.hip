@@ -1225,46 +1225,67 @@ __device__ __forceinline__ bool w_cas(uint32_t* p, uint32_t expect, uint32_t wan
 // pairs the planner needs or will need soon.
 __device__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags) {
   const unsigned long long t0 = wall_clock64();
-  for (uint32_t spin = 0;; ++spin) {
-    if ((spin & 63u) == 63u && hflags &&
-        __hip_atomic_load(&hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
-      return -1;  // host watchdog abort
-    const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
-    if (cn < hn) {
-      if (w_cas(&cc->claim_n, cn, cn + 1u)) {
-        *idx = cn;
-        return 0;
-      }
-      continue;
-    }
-    // relaxed poll (an acquire here would invalidate this XCD's L2 on every idle spin)
-    if (w_ld(&cc->stop)) {
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);
-      // the final needed head was published before `stop`: drain what is left, then exit
-      if (w_ld(&cc->claim_n) < w_ld(&cc->head_n)) continue;
-      return -1;
-    }
-    const uint32_t hs = w_ld(&cc->head_s), cs = w_ld(&cc->claim_s);
-    if (cs < hs) {
-      if (w_cas(&cc->claim_s, cs, cs + 1u)) {
-        *idx = cs;
-        return 1;
-      }
-      continue;
-    }
-    if (take_t) {
-      const uint32_t ht = w_ld(&cc->head_t), ct = w_ld(&cc->claim_t);
-      if (ct < ht) {
-        if (w_cas(&cc->claim_t, ct, ct + 1u)) {
-          *idx = ct;
-          return 2;
+  // one pass over the queues in priority order: >= 0 claimed (queue id), -1 nothing, -2 stop
+  auto scan = [&]() -> int {
+    for (;;) {
+      const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
+      if (cn < hn) {
+        if (w_cas(&cc->claim_n, cn, cn + 1u)) {
+          *idx = cn;
+          return 0;
         }
         continue;
       }
+      // relaxed poll (an acquire here would invalidate this XCD's L2 on every idle spin)
+      if (w_ld(&cc->stop)) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        // the final needed head was published before `stop`: drain what is left, then exit
+        if (w_ld(&cc->claim_n) < w_ld(&cc->head_n)) continue;
+        return -2;
+      }
+      const uint32_t hs = w_ld(&cc->head_s), cs = w_ld(&cc->claim_s);
+      if (cs < hs) {
+        if (w_cas(&cc->claim_s, cs, cs + 1u)) {
+          *idx = cs;
+          return 1;
+        }
+        continue;
+      }
+      if (take_t) {
+        const uint32_t ht = w_ld(&cc->head_t), ct = w_ld(&cc->claim_t);
+        if (ct < ht) {
+          if (w_cas(&cc->claim_t, ct, ct + 1u)) {
+            *idx = ct;
+            return 2;
+          }
+          continue;
+        }
+      }
+      return -1;
     }
-    if (wall_clock64() - t0 > 500000000ull) return -1;  // 5 s idle: safety exit
-    if (spin < 256) __builtin_amdgcn_s_sleep(2);
-    else __builtin_amdgcn_s_sleep(16);
+  };
+  // Idle: poll only the planner's publish count (one load) and rescan the queues when it moves, or
+  // every 64 polls as a safety net. Idle waves polling every head and claim word kept a few lines of
+  // the fabric hot and slowed the planner's own memory accesses (worse the more workers run).
+  uint32_t seen = w_ld(&cc->pub);
+  for (;;) {
+    const int r = scan();
+    if (r >= 0) return r;
+    if (r == -2) return -1;
+    for (uint32_t k = 0;; ++k) {
+      // host watchdog abort (pinned host memory, read over the host link: rarely)
+      if ((k & 255u) == 255u && hflags &&
+          __hip_atomic_load(&hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+        return -1;
+      if (wall_clock64() - t0 > 500000000ull) return -1;  // 5 s idle: safety exit
+      if (k < 8) __builtin_amdgcn_s_sleep(2);
+      else __builtin_amdgcn_s_sleep(16);
+      const uint32_t p = w_ld(&cc->pub);
+      if (p != seen || (k & 63u) == 63u) {
+        seen = p;
+        break;
+      }
+    }
   }
 }
 
@@ -1421,6 +1442,13 @@ WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_
     if (f.hcap >= 64u) return f;
   }
   WorkerCfg c = make(m, true);
+  // u32 LDS g-scores leave one wave per CU on a C3-sized grid; byte g-scores (tier-2 hand-off past a
+  // 62-cell detour) run 3x the waves — A* latency is the same, the startup bursts drain faster
+  // (C3 plan 585 -> 563 ms once idle workers stopped polling every queue word)
+  if (m == 1u) {
+    const WorkerCfg c2 = make(2u, true);
+    if (c2.hcap >= 64u && c2.waves >= 2u * c.waves) c = c2;
+  }
   // grids whose byte g-scores fit LDS (<= 120k cells): with many agents, trade the LDS g-scores for
   // 3x the waves (global u32 slots, L2-resident at this size)
   if (m != 0u && n_agents > 2000u && c.waves < 3u * (uint32_t)num_cu) c = make(0u, true);

@@ -183,18 +183,26 @@ __device__ void rules_init(const PlanArgs& P, const Arrays& S) {
 // the cycle), TERM / a self-loop / an agent on another cycle = not. Walks average ~2 hops on the
 // warehouse grids, against a block-wide pointer doubling over every agent. Returns false (caller
 // relabels in full) if a walk runs past `limit` hops.
+// one changed agent's successor, cleared label and CANDC (independent per agent)
+__device__ __forceinline__ void relabel_reset(const PlanArgs& P, const Arrays& S, uint32_t k) {
+  const uint32_t s = succ_of(P, S, k);
+  S.SUCC[k] = s;
+  S.ONC[k] = 0;
+  uint8_t cc = NHC_DIRTY;
+  if (s != SUCC_TERM && s != k && S.GT[k] >= 0) cc = P.nh[(uint64_t)S.GT[k] * P.nstride + S.V[s]];
+  S.CANDC[k] = cc;
+}
+
+// the walks of rules_relabel_changed, after relabel_reset of every agent in lst
+__device__ bool relabel_walks(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt, uint32_t limit);
+
 __device__ bool rules_relabel_changed(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt,
                                       uint32_t limit) {
-  for (uint32_t i = 0; i < cnt; ++i) {
-    const uint32_t k = lst[i];
-    const uint32_t s = succ_of(P, S, k);
-    S.SUCC[k] = s;
-    S.ONC[k] = 0;
-    uint8_t cc = NHC_DIRTY;
-    if (s != SUCC_TERM && s != k && S.GT[k] >= 0)
-      cc = P.nh[(uint64_t)S.GT[k] * P.nstride + S.V[s]];
-    S.CANDC[k] = cc;
-  }
+  for (uint32_t i = 0; i < cnt; ++i) relabel_reset(P, S, lst[i]);
+  return relabel_walks(P, S, lst, cnt, limit);
+}
+
+__device__ bool relabel_walks(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt, uint32_t limit) {
   for (uint32_t i = 0; i < cnt; ++i) {
     const uint32_t a = lst[i];
     if (S.ONC[a]) continue;  // labelled by an earlier walk of this loop
@@ -345,10 +353,13 @@ __device__ __forceinline__ bool plan_abort(const PlanArgs& P) {
 }
 
 // thread 0: make every entry queued so far visible to the workers (caller: after a barrier)
-__device__ __forceinline__ void coop_publish(const PlanArgs& P, const uint32_t* s_q) {
+__device__ __forceinline__ void coop_publish(const PlanArgs& P, uint32_t* s_q) {
   const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap);
   __hip_atomic_store(&P.cc->head_s, hs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&P.cc->head_n, hn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  // wake idle workers, which poll only this word (a plain agent-scope store of a new value)
+  s_q[2] += 1u;
+  __hip_atomic_store(&P.cc->pub, s_q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 constexpr unsigned long long COOP_NO_WORKER_TICKS = 5000000ull;  // 50 ms at 100 MHz: workers never started
@@ -362,7 +373,7 @@ enum : int { COOP_OK = 0, COOP_GIVE_UP = 1, COOP_RETRY = 2 };
 // safety limit (the caller exits to the host). COOP_RETRY: a pair stayed pending for 20 ms — more
 // than any A* on these grids; the caller queues the still-pending pairs again (a duplicate query
 // resolves to the same code), so a lost update can cost a retry but never a stall.
-__device__ int coop_wait(const PlanArgs& P, const Arrays& S, const uint32_t* s_q, uint32_t* s_flag, uint32_t sec) {
+__device__ int coop_wait(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_flag, uint32_t sec) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   if (tid == 0) {
     coop_publish(P, s_q);
@@ -610,7 +621,7 @@ template <bool AG, bool OC>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[2], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
+  __shared__ uint32_t s_q[3], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[24], s_tlast, s_tp;
@@ -699,6 +710,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_abort = 0;
     s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     s_q[1] = 0;  // speculative queue (coop mode)
+    s_q[2] = 0;  // publishes (coop mode)
     for (int k = 0; k < 24; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
@@ -1016,8 +1028,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         }
         if (__ballot(bad)) return false;
         __threadfence_block();
+        for (uint32_t i = lane; i < L; i += 64u) relabel_reset(P, S, ap[i]);  // lanes in parallel
+        __threadfence_block();
         uint32_t ok = 0;
-        if (lane == 0) ok = rules_relabel_changed(P, S, ap, L, 4096u) ? 1u : 0u;
+        if (lane == 0) ok = relabel_walks(P, S, ap, L, 4096u) ? 1u : 0u;
         if (!__builtin_amdgcn_readfirstlane(ok)) return false;
         if (lane == 0) s_ctl.relabel_inc += 1;
         __threadfence_block();
@@ -1684,6 +1698,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     if (P.coop) {  // last publish, then release the workers (they drain the needed queue and exit)
       coop_publish(P, s_q);
       __hip_atomic_store(&P.cc->stop, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&P.cc->pub, s_q[2] + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const uint32_t err = P.ctl->err;
     *P.ctl = s_ctl;
