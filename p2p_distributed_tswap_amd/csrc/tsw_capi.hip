@@ -61,6 +61,7 @@ struct Tunables {
   bool prefetch = true;           // TSW_NO_PREFETCH: no speculative next-hop prefetch
   uint32_t wave_rules_max = 0xFFFFFFFFu;  // TSW_WAVE_RULES_MAX: wave-0 rules rounds when n <= this
   uint32_t wide_prefetch = 8;     // TSW_WIDE_PREFETCH: resolved hops walked ahead (0 = candidates only)
+  uint32_t dag_prefetch = 2;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
   uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
@@ -89,6 +90,7 @@ struct Tunables {
     t.prefetch = getenv("TSW_NO_PREFETCH") == nullptr;
     t.wave_rules_max = (uint32_t)num("TSW_WAVE_RULES_MAX", 0, 0xFFFFFFFFl, t.wave_rules_max);
     t.wide_prefetch = (uint32_t)num("TSW_WIDE_PREFETCH", 0, 1 << 16, t.wide_prefetch);
+    t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 2, 2);
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
     t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
@@ -955,6 +957,9 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   // TSW_WAVE_RULES_MAX caps n for A/B
   P.wave_rules_max = c->tun.wave_rules_max;
   P.wide_prefetch = c->tun.wide_prefetch;
+  P.dag_prefetch = c->tun.dag_prefetch;
+  P.dist = c->d_dist;
+  P.nbmask = c->d_nbmask;
   P.pick_xy = c->d_pick_xy;
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;
@@ -1142,7 +1147,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
         if (coop) {
           const CoopCtl& cc = *c->h_cc;
           fprintf(stderr, "[k_plan] needed pairs unresolved (never queued / queued speculatively): PRE1 %u/%u RULES %u/%u "
-                  "MOVE %u/%u | fast rule-3 firings %u (code from global memory %u) | chain queries %llu of %llu\n", cc.dbg_need[0], cc.dbg_need[1], cc.dbg_need[2],
+                  "MOVE %u/%u | PRE1 never queued: assigned %u, picked up %u | chain queries %llu of %llu\n", cc.dbg_need[0], cc.dbg_need[1], cc.dbg_need[2],
                   cc.dbg_need[3], cc.dbg_need[4], cc.dbg_need[5], cc.dbg_need[6], cc.dbg_need[7],
                   (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
           fprintf(stderr, "[k_plan] worker A* ms (queries): needed %.1f (%u) spec %.1f (%u) task chains %.1f (%u)\n",

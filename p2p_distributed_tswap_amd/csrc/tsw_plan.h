@@ -49,6 +49,9 @@ struct PlanArgs {
   uint32_t f_lds;               // F1/F2 carved in LDS although the agent arrays are global
   uint32_t wave_rules_max;      // rules rounds run in wave 0 alone when n <= this
   uint32_t wide_prefetch;       // 0: off; else also (succ cell, goal) of every agent, path walked this many hops ahead
+  uint32_t dag_prefetch;        // walk-ahead also queues the shortest-path successors of the first unresolved cell
+  const uint16_t* dist;         // K1 distance tables (nstride entries per slot), for dag_prefetch
+  const uint8_t* nbmask;        // per cell: bit d = neighbour in direction d is free
   uint32_t* v;
   uint32_t* g;
   uint8_t* st;

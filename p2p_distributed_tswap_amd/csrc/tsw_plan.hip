@@ -323,8 +323,11 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
       S.NHC[k] = code;
     } else {
       if (P.dbg && P.coop && (code == NH_UNKNOWN || code == NH_PENDING_S)) {
-        const uint32_t grp = sec == SEC_PRE1 ? 0u : sec == SEC_RULES ? 1u : sec == SEC_MOVE ? 2u : 3u;
+        const uint32_t grp = sec == SEC_PRE1 ? 0u : sec == SEC_RULES ? 1u : 2u;
         atomicAdd(&P.cc->dbg_need[2u * grp + (code == NH_PENDING_S ? 1u : 0u)], 1u);
+        // PRE1, never queued: assigned a task / picked up in this step's ASSIGN (DEC tag, diagnostics)
+        if (sec == SEC_PRE1 && code == NH_UNKNOWN && (S.DEC[k] & 0x40u))
+          atomicAdd(&P.cc->dbg_need[(S.DEC[k] & 1u) ? 7u : 6u], 1u);
       }
       enqueue_pair(P, v, g, tab, s_q);  // no-op if already queued (PENDING)
       atomicAdd(s_need, 1u);
@@ -529,11 +532,12 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (spec_full(P, s_q)) break;
     // heading to a pickup: the pair the state machine needs on arrival (goal := delivery,
-    // tswap.rs:113-118) is known since the assignment — (pickup cell, delivery goal)
+    // tswap.rs:113-118) is known since the assignment — (arrival cell, delivery goal). The arrival
+    // cell is the agent's current goal: rule-3/4 swaps may have traded the task's pickup cell away.
     if (P.mode != MODE_STEP && P.m > 0 && P.st[k] == ST_TO_PICKUP) {
       const int32_t tk = P.task[k];
       if (tk >= 0 && (uint32_t)tk < P.m) {
-        const uint32_t pc = P.pick[tk], dc = P.dlv[tk];
+        const uint32_t pc = S.G[k], dc = P.dlv[tk];
         const int32_t dt = P.goal_tab[dc];
         if (dt >= 0 && pc != dc && P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) prefetch_pair(P, pc, dc, dt, s_q);
       }
@@ -545,11 +549,42 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
     uint32_t u = step_cell(S.V[k], c, P.W);
     for (uint32_t h = 0; h < hops && u != S.G[k]; ++h) {
       const uint8_t cu = P.nh[(uint64_t)tab * P.nstride + u];
-      if (cu == NH_UNKNOWN) {
-        prefetch_pair(P, u, S.G[k], tab, s_q);
+      if (cu == NH_UNKNOWN || cu == NH_PENDING || cu == NH_PENDING_S) {
+        if (cu == NH_UNKNOWN) prefetch_pair(P, u, S.G[k], tab, s_q);
+        // one level past it: whichever neighbour u's code picks lies one step closer to the goal
+        // (every get_path is a shortest path), so queue those too — the agent's path then resolves
+        // two cells per A* latency instead of one
+        if (P.dag_prefetch) {
+          const uint16_t* dt = P.dist + (uint64_t)tab * P.nstride;
+          const uint8_t* ht = P.nh + (uint64_t)tab * P.nstride;
+          const uint32_t g = S.G[k];
+          // the shortest-path successors of cell x (neighbours one step closer to g), queued; up to
+          // two of them returned for the next level
+          auto level = [&](uint32_t x, uint32_t* out) -> uint32_t {
+            const uint32_t dx = dt[x];
+            const uint8_t nb = P.nbmask[x];
+            uint32_t no = 0;
+#pragma unroll
+            for (uint32_t d = 0; d < 4u; ++d) {
+              if (!((nb >> d) & 1u)) continue;
+              const uint32_t w = step_cell(x, d, P.W);
+              if (w == g || (uint32_t)dt[w] + 1u != dx) continue;
+              const uint8_t cw = ht[w];
+              if (cw == NH_UNKNOWN) prefetch_pair(P, w, g, tab, s_q);
+              if (cw > NH_STAY && no < 2u) out[no++] = w;  // unresolved: its successors are open too
+            }
+            return no;
+          };
+          uint32_t l1[2], l2[2];
+          const uint32_t n1 = level(u, l1);
+          if (P.dag_prefetch > 1u) {
+            if (n1 > 0u) level(l1[0], l2);
+            if (n1 > 1u) level(l1[1], l2);
+          }
+        }
         break;
       }
-      if (cu >= NH_STAY) break;  // pending, or a stay code
+      if (cu >= NH_STAY) break;  // a stay code
       u = step_cell(u, cu, P.W);
     }
   }
@@ -786,6 +821,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
               if (st == ST_TO_PICKUP) {
                 st = ST_TO_DELIVERY;
                 ++s_npick;
+                if (P.dbg) S.DEC[ai] = 0x41;  // diagnostics tag (MOVE re-initialises DEC)
                 const int32_t tk = P.task[ai];
                 if (tk >= 0) {
                   const uint32_t ng = P.dlv[tk];
@@ -830,6 +866,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                 P.task[ai] = (int32_t)t;
                 P.st[ai] = ST_TO_PICKUP;
                 ++s_nassign;
+                if (P.dbg) S.DEC[ai] = 0x40;
                 const uint32_t ng = P.pick[t];
                 S.G[ai] = ng;
                 S.GT[ai] = P.goal_tab[ng];
