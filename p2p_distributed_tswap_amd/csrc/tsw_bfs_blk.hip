@@ -93,10 +93,15 @@ __device__ __forceinline__ uint32_t ct_slot(uint32_t lane, uint32_t j) {
 
 }  // namespace
 
-// LDS dwords of one wave; must match the carve in k_bfs_blk.
+// LDS dwords of one wave; must match the carve in k_bfs_blk: V (nbp rounded to even u64), flags,
+// then the list / run-table / staging region LS, 16-B aligned (every part is a multiple of 4 dwords).
 __host__ __device__ __forceinline__ uint32_t blk_bfs_words(uint32_t nbp, uint32_t nfk, uint32_t cap) {
-  const uint32_t ls = 2u * cap < CT_U16 ? CT_U16 : 2u * cap;  // u16 entries: two lists or the run table
-  return 2u * nbp + 2u * nfk + ((ls + 1u) >> 1);
+  const uint32_t ls = 2u * cap < CT_U16 ? CT_U16 : 2u * cap;  // u16 entries: two lists, run table, staging
+  return 2u * ((nbp + 1u) & ~1u) + 2u * nfk + ((ls + 7u) >> 3) * 4u;
+}
+// u64 words of the workgroup's shared part (FR u64 + AB u32), rounded to 16 B
+__host__ __device__ __forceinline__ uint32_t blk_shared_u64(uint32_t nbp) {
+  return (nbp + (nbp + 1u) / 2u + 1u) & ~1u;
 }
 
 __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
@@ -110,9 +115,9 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   uint32_t* FL;  // 2 * nfk interleaved flag dwords: block t -> dword t & kmask, bit t >> klog
   uint16_t* LS;  // 2 * cap list entries / decode run table
   {
-    uint32_t* b = reinterpret_cast<uint32_t*>(smem64 + nbp + (nbp + 1u) / 2u) + wv * blk_bfs_words(nbp, nfk, cap);
+    uint32_t* b = reinterpret_cast<uint32_t*>(smem64 + blk_shared_u64(nbp)) + wv * blk_bfs_words(nbp, nfk, cap);
     V = reinterpret_cast<uint64_t*>(b);
-    FL = b + 2u * nbp;
+    FL = b + 2u * ((nbp + 1u) & ~1u);
     LS = reinterpret_cast<uint16_t*>(FL + 2u * nfk);
   }
   for (uint32_t t = tid; t < nbp; t += blockDim.x) {
@@ -438,10 +443,10 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         rs &= rs - 1u;
       }
     };
-    auto decode = [&](const Word& cu) {
-      const uint32_t y = cu.y, cw = cu.cw, r = cu.r, p0 = cu.p0, vis = cu.vis, wl = cu.wl, f0 = cu.f0;
+    // decode of this lane's word into pk (two u16 per dword); false when the word has no visited cell
+    auto decode = [&](const Word& cu, uint32_t* pk) {
+      const uint32_t r = cu.r, p0 = cu.p0, vis = cu.vis, wl = cu.wl, f0 = cu.f0;
       const uint32_t rsw = f0 & ~(f0 << 1);
-      uint32_t pk[16];
       if (vis != 0u) {
         // runs 1..4: branch-free with the prefetched anchors (rows past the last run are never
         // looked up); runs 5..16 (rare) load their anchors here
@@ -473,9 +478,12 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) pk[j] = 0xFFFFFFFFu;
       }
-      const uint32_t x0 = cw << 5;
+    };
+    // lane-strided write-out (tables not 16-B aligned): the row word goes straight to HBM
+    auto put_direct = [&](const Word& cu, const uint32_t* pk) {
+      const uint32_t x0 = cu.cw << 5;
       const uint32_t cnt = min(32u, W - x0);
-      uint16_t* dst = D + (uint64_t)y * W + x0;
+      uint16_t* dst = D + (uint64_t)cu.y * W + x0;
       if (A.vec16 && cnt == 32u) {
         uint4* q = reinterpret_cast<uint4*>(dst);
         q[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
@@ -488,21 +496,77 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
           if (b < cnt) dst[b] = (uint16_t)(pk[b >> 1] >> ((b & 1u) * 16u));
       }
     };
+    // Staged write-out of the wave's 64 consecutive words kb..kb+63 (valid: this lane's word exists).
+    // Consecutive row words tile the row-major table, so each half-wave's 32 words are ONE contiguous
+    // cell range [cs, ce) (<= 1024 cells): the half's lanes put their cells into LS at (cell - base),
+    // base = cs rounded down to 8 cells, then the whole wave stores 16-B chunks of that range — lane q
+    // takes chunk q, so every store instruction covers 1 KB contiguous (a lane-strided 16-B pattern
+    // measured 11x slower than coalesced stores on gfx950: scripts/calib_write.hip). Chunks cut by the
+    // range ends (neighbouring halves own the rest) are written cell by cell.
+    auto put_staged = [&](const Word& cu, const uint32_t* pk, bool valid, uint32_t kb) {
+      const uint32_t x0 = cu.cw << 5;
+      const uint32_t cnt = valid ? min(32u, W - x0) : 0u;
+      const uint32_t cb = cu.y * W + x0;
+#pragma unroll
+      for (uint32_t hh = 0; hh < 2u; ++hh) {
+        const uint32_t fl = 32u * hh;
+        if (kb + fl >= nwords) break;  // wave-uniform
+        const uint32_t ll = min(fl + 31u, nwords - 1u - kb);
+        const uint32_t cs = (uint32_t)__builtin_amdgcn_readlane((int)cb, (int)fl);
+        const uint32_t ce = (uint32_t)__builtin_amdgcn_readlane((int)(cb + cnt), (int)ll);
+        const uint32_t base = cs & ~7u;
+        if (valid && (lane >> 5) == hh) {
+          const uint32_t off = cb - base;
+          if ((W & 31u) == 0u) {  // word starts 64-B aligned in the staging buffer
+            uint4* q = reinterpret_cast<uint4*>(LS + off);
+            q[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            q[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+            q[2] = make_uint4(pk[8], pk[9], pk[10], pk[11]);
+            q[3] = make_uint4(pk[12], pk[13], pk[14], pk[15]);
+          } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 32u; ++b)
+              if (b < cnt) LS[off + b] = (uint16_t)(pk[b >> 1] >> ((b & 1u) * 16u));
+          }
+        }
+        lds_sync();  // one wave: the DS unit runs its instructions in order
+        const uint32_t nch = (ce - base + 7u) >> 3;
+        for (uint32_t q = lane; q < nch; q += 64u) {
+          const uint32_t c0 = base + 8u * q;
+          if (c0 >= cs && c0 + 8u <= ce) {
+            *reinterpret_cast<uint4*>(D + c0) = *reinterpret_cast<const uint4*>(LS + 8u * q);
+          } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 8u; ++b)
+              if (c0 + b >= cs && c0 + b < ce) D[c0 + b] = LS[8u * q + b];
+          }
+        }
+        lds_sync();  // staging reads issued before the next half / the next run table overwrites LS
+      }
+    };
+    auto emit = [&](const Word& cu, bool valid, uint32_t kb) {
+      uint32_t pk[16];
+      if (valid) decode(cu, pk);
+      if (A.stage) put_staged(cu, pk, valid, kb);
+      else if (valid) put_direct(cu, pk);
+    };
     // four words in flight per lane (ring w0..w3, fetch distance 4): a decode waits on loads
-    // issued three decodes earlier, enough to cover L2 latency at this residency
+    // issued three decodes earlier, enough to cover L2 latency at this residency. The loop is
+    // wave-uniform (the staged write-out is a wave-wide exchange); lanes past the end idle.
     Word w0{}, w1{}, w2{}, w3{};
     if (lane < nwords) fetch(lane, w0);
     if (lane + 64u < nwords) fetch(lane + 64u, w1);
     if (lane + 128u < nwords) fetch(lane + 128u, w2);
     if (lane + 192u < nwords) fetch(lane + 192u, w3);
-    for (uint32_t k = lane; k < nwords; k += 256u) {
-      decode(w0);
+    for (uint32_t kb = 0; kb < nwords; kb += 256u) {
+      const uint32_t k = kb + lane;
+      emit(w0, k < nwords, kb);
       if (k + 256u < nwords) fetch(k + 256u, w0);
-      if (k + 64u < nwords) decode(w1);
+      if (kb + 64u < nwords) emit(w1, k + 64u < nwords, kb + 64u);
       if (k + 320u < nwords) fetch(k + 320u, w1);
-      if (k + 128u < nwords) decode(w2);
+      if (kb + 128u < nwords) emit(w2, k + 128u < nwords, kb + 128u);
       if (k + 384u < nwords) fetch(k + 384u, w2);
-      if (k + 192u < nwords) decode(w3);
+      if (kb + 192u < nwords) emit(w3, k + 192u < nwords, kb + 192u);
       if (k + 448u < nwords) fetch(k + 448u, w3);
     }
     lds_sync();  // the next goal re-initialises this wave's LDS
@@ -529,7 +593,7 @@ uint32_t bfs_blk_klog(uint32_t nbp) {
 
 uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds) {
   const size_t per_wave = (size_t)blk_bfs_words(nbp, 1u << bfs_blk_klog(nbp), cap) * 4u;
-  const size_t shared = (size_t)(nbp + (nbp + 1u) / 2u) * 8u;  // FR u64 + AB u32
+  const size_t shared = (size_t)blk_shared_u64(nbp) * 8u;  // FR u64 + AB u32
   if (max_lds <= 0 || shared + per_wave > (size_t)max_lds) return 0;
   return (uint32_t)std::min<size_t>(16u, ((size_t)max_lds - shared) / per_wave);
 }
@@ -540,7 +604,7 @@ hipError_t launch_bfs_blk(const BlkBfsArgs& A0, int max_lds, int num_cu, hipStre
   A.klog = bfs_blk_klog(A.nbp);
   A.bp_magic = (uint32_t)((0xFFFFFFFFull + A.Bp) / A.Bp);  // ceil(2^32 / Bp): exact p / Bp for p*Bp < 2^32
   const size_t per_wave = (size_t)blk_bfs_words(A.nbp, 1u << A.klog, A.cap) * 4u;
-  const size_t shared = (size_t)(A.nbp + (A.nbp + 1u) / 2u) * 8u;  // FR u64 + AB u32
+  const size_t shared = (size_t)blk_shared_u64(A.nbp) * 8u;  // FR u64 + AB u32
   const uint32_t nwv = std::min<uint32_t>(A.max_waves, bfs_blk_waves_per_block(A.nbp, A.cap, max_lds));
   if (nwv == 0 || A.nbp > 0x10000u || A.cap > 0x8000u) return hipErrorInvalidValue;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cu, (A.k + nwv - 1u) / nwv));

@@ -54,6 +54,7 @@ struct Tunables {
   uint32_t bfs_waves = 16;        // TSW_BFS_WAVES: waves per K1 workgroup cap
   bool bfs_order = true;          // TSW_BFS_ORDER=0: keep the caller's goal order (no LPT)
   bool bfs_prof = false;          // TSW_BFS_PROF: print K1 cycle split per launch
+  bool bfs_nostage = false;       // TSW_BFS_NOSTAGE: k_bfs_blk writes rows lane-strided (no LDS staging)
   uint32_t wave_hcap = 0;         // TSW_ASTAR_WAVE_HCAP: k_astar_wave LDS heap entries (0 = default)
   int astar_global_gs = -1;       // TSW_ASTAR_GLOBAL_GS: -1 auto, 0 LDS g-scores, 1 global slots
   bool astar_tier2 = true;        // TSW_ASTAR_NO_TIER2: skip the LDS-heap/global-g second tier
@@ -83,6 +84,7 @@ struct Tunables {
     t.bfs_waves = (uint32_t)num("TSW_BFS_WAVES", 1, 16, t.bfs_waves);
     t.bfs_order = num("TSW_BFS_ORDER", 0, 1, 1) != 0;
     t.bfs_prof = getenv("TSW_BFS_PROF") != nullptr;
+    t.bfs_nostage = getenv("TSW_BFS_NOSTAGE") != nullptr;
     t.wave_hcap = (uint32_t)num("TSW_ASTAR_WAVE_HCAP", 4, 1 << 20, 0);
     t.astar_global_gs = (int)num("TSW_ASTAR_GLOBAL_GS", 0, 1, -1);
     t.astar_tier2 = getenv("TSW_ASTAR_NO_TIER2") == nullptr;
@@ -636,6 +638,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     A.work = &c->d_stat->work;
     A.err = &c->d_stat->err;
     A.vec16 = vec16 ? 1u : 0u;
+    A.stage = (dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u && !c->tun.bfs_nostage) ? 1u : 0u;
     A.max_waves = nbw;
     A.scratch_waves = std::min(c->wave_scratch, c->wlg_waves);
     A.prof = (uint64_t*)bfs_prof_buf(c);

@@ -56,6 +56,8 @@ struct BlkBfsArgs {
   uint32_t* work;         // goal dequeue counter (zeroed before the launch)
   uint32_t* err;
   uint32_t vec16;         // 16-B stores allowed (W % 8 == 0, 16-B aligned tables)
+  uint32_t stage;         // tables 16-B aligned (dist, dstride % 8 == 0): decoded rows leave through an
+                          // LDS staging pass as coalesced 16-B stores (any W)
   uint32_t max_waves;
   uint64_t scratch_waves;
   uint64_t* prof;         // optional: [bfs cycles, decode cycles, levels, chunks] summed over waves
