@@ -18,8 +18,9 @@ Extra objects on the line:
                 on the library's stream, tsw_get_stats), algorithmic bytes per launch, and the
                 PMC traffic per launch from profiles/<PROFILE_TAG>/pmc.json — only when that file
                 was measured on THIS workload (same algorithmic bytes per launch), else null.
-  latency       K3 and k_plan against their latency floors (they are serial-dependency bound,
-                not bandwidth bound; see DESIGN.md "Latency rooflines").
+  latency       k_plan against its latency floor (bound "latency"): rules / movement rounds x the
+                measured floor per round shape (tsw_probe_round_floors), beside the achieved section
+                time; the K3 wait time (the A* critical path) beside it. DESIGN.md "Latency roofline".
   bfs           K1 alone on a den520d-like 256x257 cave, 10,000 distinct goals (configs[3]),
                 cells/s and fraction of the 8 TB/s HBM peak (algorithmic bytes).
   cpu_baseline  the oracle (faithful single-thread C restatement of tswap.rs) planning a bounded
@@ -87,6 +88,47 @@ def bfs_bytes_per_goal(w: int, h: int, with_nh: bool) -> int:
     + the obstacle bitmap read."""
     cells = w * h
     return cells * 2 + (cells if with_nh else 0) + (cells + 7) // 8
+
+
+# block-wide passes every timestep makes outside the rounds (ASSIGN compaction, PRE1 and PRE2 refresh,
+# movement init, RECORD): the per-step part of k_plan's floor
+STEP_PASSES = 5
+
+
+def latency_roofline(st: dict, us_wave: float, us_pass: float) -> dict:
+    """k_plan against its latency floor (DESIGN.md "Latency roofline"). k_plan runs tswap_step's two
+    sequential scans as rounds of one workgroup; a round's floor is the dependent chain its shape
+    cannot avoid, measured live by tsw_probe_round_floors: a wave-0 rules firing (LDS load, ballot,
+    first lane, readlane, store) and a block-wide pass (LDS exchange + barrier; a movement round is
+    three). floor = rule_rounds * wave + (3 * move_rounds + STEP_PASSES * steps) * pass. achieved =
+    section device time minus the time the planner waited for K3 (exact A* on the concurrent workers:
+    the other critical path, reported beside it)."""
+    sec, wsec = st["plan_section_ms"], st["coop_wait_sec_ms"]
+    rr, mr, steps = st["rule_rounds"], st["move_rounds"], st["steps"]
+
+    def part(rounds, us_round, achieved_ms):
+        floor_ms = rounds * us_round / 1e3
+        return {"rounds": int(rounds), "rounds_per_step": round(rounds / max(steps, 1), 2),
+                "floor_us_per_round": round(us_round, 4),
+                "achieved_us_per_round": round(achieved_ms * 1e3 / max(rounds, 1), 4),
+                "floor_ms": round(floor_ms, 3), "achieved_ms": round(achieved_ms, 3),
+                "frac": round(floor_ms / achieved_ms, 4) if achieved_ms > 0 else None}
+
+    rules = part(rr, us_wave, sec[2] - wsec[2])
+    move = part(mr, 3.0 * us_pass, sec[4] - wsec[4])
+    achieved = st["walker_ms"] - st["coop_wait_ms"]
+    floor = rules["floor_ms"] + move["floor_ms"] + STEP_PASSES * steps * us_pass / 1e3
+    return {
+        "k_plan": {"bound": "latency", "unit": "ms", "floor_ms": round(floor, 3), "achieved_ms": round(achieved, 3),
+                   "frac": round(floor / achieved, 4) if achieved > 0 else None,
+                   "steps": int(steps), "step_passes": STEP_PASSES},
+        "rules": rules,
+        "movement": move,
+        "probe": {"us_wave_round": round(us_wave, 4), "us_block_pass": round(us_pass, 4),
+                  "block": int(st.get("plan_block", 0))},
+        "k3_wait_ms": round(st["coop_wait_ms"], 3),
+        "k3_waits": int(st["coop_waits"]),
+    }
 
 
 def host_cpu_model() -> str:
@@ -204,6 +246,9 @@ def main():
         st = planner.stats()
         dt_max = allmax(dt)
         value = allsum(float(agent_steps)) / dt_max
+        # latency floors of k_plan's round shapes on its own workgroup size (tsw_probe.hip), measured
+        # after the timed region
+        us_wave, us_pass = planner.probe_round_floors(0)
         planner.close()
 
         # kernel classes inside the timed region (device time from HIP events on the library stream)
@@ -244,14 +289,7 @@ def main():
                      "construction and their binding limit is latency (see `latency`). K1 (bfs.roofline) is the "
                      "HBM-bound kernel." if dom != "K1" else None),
         }
-        latency = {
-            "k3_pops": st.get("astar_pops", 0),
-            "k3_critical_pops": st.get("astar_crit_pops", 0),
-            "k3_ms": round(st["astar_ms"], 3),
-            "k_plan_ms": round(st["walker_ms"], 3),
-            "plan_exits": st["plan_exits"],
-            "rule_rounds": st["rule_rounds"],
-        }
+        latency = latency_roofline(st, us_wave, us_pass)
 
     # K1 BFS alone, den520d-like, 10k distinct goals (configs[3]); rank-local shard of the goals
     bfs = None

@@ -214,11 +214,19 @@ typedef struct {
     uint64_t coop_waits_sec[8];
     /* rules-phase cycle relabels: block-wide pointer doubling / incremental walks */
     uint64_t relabels_full, relabels_inc;
+    uint64_t move_rounds;       /* decidability rounds run by the movement phase */
+    uint32_t plan_block;        /* workgroup size of the last plan kernel launch */
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);
 /* Enable/disable HIP-event timing around kernels (default on). */
 int tsw_set_timing(tsw_ctx *ctx, int enabled);
+/* Measurement probe (not part of the reference interface): latency floors of the plan kernel's
+ * round shapes on a `block`-thread workgroup (0 = the last plan's), HIP-event timed on the context
+ * stream. out[0] = us per wave-0 rules firing chain (LDS load of 64 candidates, ballot, first lane,
+ * readlane, that lane's store), out[1] = us per block-wide pass (LDS exchange + barrier; a movement
+ * round is three). bench.py reports k_plan against rule_rounds * out[0] + 3 * move_rounds * out[1]. */
+int tsw_probe_round_floors(tsw_ctx *ctx, uint32_t block, double *out);
 
 #ifdef __cplusplus
 }

@@ -91,6 +91,7 @@ class Stats(ctypes.Structure):
         ("coop_waits", ctypes.c_uint64), ("coop_wait_ms", ctypes.c_double),
         ("coop_wait_sec_ms", ctypes.c_double * 8), ("coop_waits_sec", ctypes.c_uint64 * 8),
         ("relabels_full", ctypes.c_uint64), ("relabels_inc", ctypes.c_uint64),
+        ("move_rounds", ctypes.c_uint64), ("plan_block", ctypes.c_uint32),
     ]
 
     def as_dict(self):
@@ -107,7 +108,7 @@ EXPORTED_SYMBOLS = (
     "tsw_create", "tsw_destroy", "tsw_last_error", "tsw_plan_mapd", "tsw_plan_mapd_trace",
     "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables", "tsw_dist_tables_device",
     "tsw_import_tables_device", "tsw_next_hop_tables", "tsw_next_hop_tables_device", "tsw_import_next_hops_device",
-    "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing",
+    "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing", "tsw_probe_round_floors",
 )
 
 _lib = None
@@ -146,10 +147,11 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_get_stats.argtypes = [vp, P(Stats)]
     lib.tsw_reset_stats.argtypes = [vp]
     lib.tsw_set_timing.argtypes = [vp, ctypes.c_int]
+    lib.tsw_probe_round_floors.argtypes = [vp, ctypes.c_uint32, P(ctypes.c_double)]
     for name in ("tsw_plan_mapd", "tsw_plan_mapd_trace", "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables",
                  "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_clear_tables", "tsw_next_hop_tables",
                  "tsw_next_hop_tables_device", "tsw_import_next_hops_device", "tsw_get_stats", "tsw_reset_stats",
-                 "tsw_set_timing"):
+                 "tsw_set_timing", "tsw_probe_round_floors"):
         getattr(lib, name).restype = ctypes.c_int
     _lib = lib
     return lib
@@ -345,6 +347,13 @@ class Planner:
 
     def reset_stats(self):
         self._check(self._lib.tsw_reset_stats(self._ctx))
+
+    def probe_round_floors(self, block: int = 0) -> tuple:
+        """(us per wave-0 rules firing chain, us per block-wide pass) of the plan kernel's round
+        shapes on a `block`-thread workgroup (0 = the last plan's): its latency floors (bench.py)."""
+        out = (ctypes.c_double * 2)()
+        self._check(self._lib.tsw_probe_round_floors(self._ctx, block, out))
+        return float(out[0]), float(out[1])
 
     def set_timing(self, on: bool):
         self._check(self._lib.tsw_set_timing(self._ctx, 1 if on else 0))

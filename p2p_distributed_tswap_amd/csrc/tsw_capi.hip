@@ -62,7 +62,7 @@ struct Tunables {
   bool prefetch = true;           // TSW_NO_PREFETCH: no speculative next-hop prefetch
   uint32_t wave_rules_max = 0xFFFFFFFFu;  // TSW_WAVE_RULES_MAX: wave-0 rules rounds when n <= this
   uint32_t wide_prefetch = 8;     // TSW_WIDE_PREFETCH: resolved hops walked ahead (0 = candidates only)
-  uint32_t dag_prefetch = 2;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell
+  uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
   uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
@@ -92,7 +92,7 @@ struct Tunables {
     t.prefetch = getenv("TSW_NO_PREFETCH") == nullptr;
     t.wave_rules_max = (uint32_t)num("TSW_WAVE_RULES_MAX", 0, 0xFFFFFFFFl, t.wave_rules_max);
     t.wide_prefetch = (uint32_t)num("TSW_WIDE_PREFETCH", 0, 1 << 16, t.wide_prefetch);
-    t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 2, 2);
+    t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 16, t.dag_prefetch);
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
     t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
@@ -1061,6 +1061,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     {
       Timer t(c, CAT_WALK);
       HIPCHK(launch_plan(P, lds, block, c->s));
+      c->st.plan_block = block;
     }
     c->st.walker_launches++;
     if (coop) {
@@ -1137,6 +1138,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     if (k.status == PLAN_DONE) {
       c->chase_id = k.chase_id;
       c->st.rule_rounds += k.rule_rounds;
+      c->st.move_rounds += k.move_rounds;
       if (c->tun.plan_debug) {
         unsigned long long tk[24];
         HIPCHK(hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost));
@@ -1919,6 +1921,16 @@ int tsw_set_timing(tsw_ctx* c, int enabled) {
   if (!c) return TSW_EINVAL;
   resolve_timing(c);
   c->timing = enabled != 0;
+  return TSW_OK;
+}
+
+int tsw_probe_round_floors(tsw_ctx* c, uint32_t block, double* out) {
+  if (!c || !out) return TSW_EINVAL;
+  if (block == 0) block = c->st.plan_block ? c->st.plan_block : 1024u;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->s));
+  HIPCHK(probe_round_floors(block, std::max<uint32_t>(c->acap ? (uint32_t)c->acap : 1024u, 64u), c->s, &out[0],
+                            &out[1]));
   return TSW_OK;
 }
 

@@ -150,4 +150,8 @@ hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
                                   uint32_t qcap, hipStream_t s);
 
+// Latency floors of k_plan's round shapes (tsw_probe.hip): us per wave-0 rules firing chain and per
+// block-wide pass (LDS exchange + barrier) on a `block`-thread workgroup.
+hipError_t probe_round_floors(uint32_t block, uint32_t n, hipStream_t s, double* us_wave_round, double* us_block_pass);
+
 }  // namespace tsw

@@ -551,35 +551,47 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
       const uint8_t cu = P.nh[(uint64_t)tab * P.nstride + u];
       if (cu == NH_UNKNOWN || cu == NH_PENDING || cu == NH_PENDING_S) {
         if (cu == NH_UNKNOWN) prefetch_pair(P, u, S.G[k], tab, s_q);
-        // one level past it: whichever neighbour u's code picks lies one step closer to the goal
-        // (every get_path is a shortest path), so queue those too — the agent's path then resolves
-        // two cells per A* latency instead of one
+        // levels past it: whichever neighbour u's code picks lies one step closer to the goal
+        // (every get_path is a shortest path), so the shortest-path DAG ahead of u is where the
+        // agent goes next. Its cells are queued level by level (frontier capped at DAG_WIDTH; a
+        // resolved cell contributes only the cell its code points at), so the agent's path
+        // resolves several cells per A* latency instead of one.
         if (P.dag_prefetch) {
+          constexpr uint32_t DAG_WIDTH = 4;
           const uint16_t* dt = P.dist + (uint64_t)tab * P.nstride;
           const uint8_t* ht = P.nh + (uint64_t)tab * P.nstride;
           const uint32_t g = S.G[k];
-          // the shortest-path successors of cell x (neighbours one step closer to g), queued; up to
-          // two of them returned for the next level
-          auto level = [&](uint32_t x, uint32_t* out) -> uint32_t {
-            const uint32_t dx = dt[x];
-            const uint8_t nb = P.nbmask[x];
-            uint32_t no = 0;
+          uint32_t fr[DAG_WIDTH], nf = 1;
+          fr[0] = u;
+          for (uint32_t lv = 0; lv < P.dag_prefetch && nf > 0u; ++lv) {
+            uint32_t nx[DAG_WIDTH], nn = 0;
+            auto add = [&](uint32_t w) {
+              for (uint32_t i = 0; i < nn; ++i)
+                if (nx[i] == w) return;
+              if (nn < DAG_WIDTH) nx[nn++] = w;
+            };
+            for (uint32_t i = 0; i < nf; ++i) {
+              const uint32_t x = fr[i];
+              const uint8_t cx = ht[x];
+              if (cx < NH_STAY) {  // resolved: the agent's path continues at one cell
+                const uint32_t w = step_cell(x, cx, P.W);
+                if (w != g) add(w);
+                continue;
+              }
+              if (cx == NH_STAY) continue;
+              const uint32_t dx = dt[x];
+              const uint8_t nb = P.nbmask[x];
 #pragma unroll
-            for (uint32_t d = 0; d < 4u; ++d) {
-              if (!((nb >> d) & 1u)) continue;
-              const uint32_t w = step_cell(x, d, P.W);
-              if (w == g || (uint32_t)dt[w] + 1u != dx) continue;
-              const uint8_t cw = ht[w];
-              if (cw == NH_UNKNOWN) prefetch_pair(P, w, g, tab, s_q);
-              if (cw > NH_STAY && no < 2u) out[no++] = w;  // unresolved: its successors are open too
+              for (uint32_t d = 0; d < 4u; ++d) {
+                if (!((nb >> d) & 1u)) continue;
+                const uint32_t w = step_cell(x, d, P.W);
+                if (w == g || (uint32_t)dt[w] + 1u != dx) continue;
+                if (ht[w] == NH_UNKNOWN) prefetch_pair(P, w, g, tab, s_q);
+                add(w);
+              }
             }
-            return no;
-          };
-          uint32_t l1[2], l2[2];
-          const uint32_t n1 = level(u, l1);
-          if (P.dag_prefetch > 1u) {
-            if (n1 > 0u) level(l1[0], l2);
-            if (n1 > 1u) level(l1[1], l2);
+            for (uint32_t i = 0; i < nn; ++i) fr[i] = nx[i];
+            nf = nn;
           }
         }
         break;
