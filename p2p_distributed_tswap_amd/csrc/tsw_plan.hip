@@ -502,12 +502,21 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
 // rules_prefetch restricted to the agents a firing changed (rule 3: b and s, rule 4: the cycle):
 // only their goals, hence their next hops and successors, moved, so only their pairs are new.
 // After rules_init (SUCC valid).
+__device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab,
+                                  uint32_t hops);
+__device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab);
+
 __device__ __forceinline__ void prefetch_changed(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t k) {
   if (spec_full(P, s_q)) return;
   const int32_t tab = S.GT[k];
   if (tab < 0) return;
   const uint8_t c = S.NHC[k];
-  if (c < NH_STAY && S.V[k] != S.G[k]) {
+  if (S.V[k] != S.G[k] && (P.prefetch_ext & 4u)) {
+    // the agent's new path: walked ahead (and the DAG past its first unresolved cell) now, a step
+    // before the next step's walk-ahead would queue it
+    if (c < NH_STAY) walk_prefetch(P, s_q, step_cell(S.V[k], c, P.W), S.G[k], tab, P.wide_prefetch ? P.wide_prefetch : 1u);
+    else if (c > NH_STAY && P.dag_prefetch) dag_prefetch(P, s_q, S.V[k], S.G[k], tab);
+  } else if (c < NH_STAY && S.V[k] != S.G[k]) {
     const uint32_t u = step_cell(S.V[k], c, P.W);
     if (u != S.G[k] && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) prefetch_pair(P, u, S.G[k], tab, s_q);
   }
@@ -524,9 +533,75 @@ __device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t
   __syncthreads();
 }
 
+// The shortest-path DAG toward goal g past cell u (u's own pair is queued by the caller): whichever
+// neighbour u's code picks lies one step closer to the goal (every get_path is a shortest path), so
+// the DAG ahead of u is where the agent goes next. Its cells are queued level by level (frontier
+// capped at DAG_WIDTH; a resolved cell contributes only the cell its code points at), so a path
+// resolves several cells per A* latency instead of one.
+__device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab) {
+  constexpr uint32_t DAG_WIDTH = 4;
+  const uint16_t* dt = P.dist + (uint64_t)tab * P.nstride;
+  const uint8_t* ht = P.nh + (uint64_t)tab * P.nstride;
+  uint32_t fr[DAG_WIDTH], nf = 1;
+  fr[0] = u;
+  for (uint32_t lv = 0; lv < P.dag_prefetch && nf > 0u; ++lv) {
+    uint32_t nx[DAG_WIDTH], nn = 0;
+    auto add = [&](uint32_t w) {
+      for (uint32_t i = 0; i < nn; ++i)
+        if (nx[i] == w) return;
+      if (nn < DAG_WIDTH) nx[nn++] = w;
+    };
+    for (uint32_t i = 0; i < nf; ++i) {
+      const uint32_t x = fr[i];
+      const uint8_t cx = ht[x];
+      if (cx < NH_STAY) {  // resolved: the agent's path continues at one cell
+        const uint32_t w = step_cell(x, cx, P.W);
+        if (w != g) add(w);
+        continue;
+      }
+      if (cx == NH_STAY) continue;
+      const uint32_t dx = dt[x];
+      const uint8_t nb = P.nbmask[x];
+#pragma unroll
+      for (uint32_t d = 0; d < 4u; ++d) {
+        if (!((nb >> d) & 1u)) continue;
+        const uint32_t w = step_cell(x, d, P.W);
+        if (w == g || (uint32_t)dt[w] + 1u != dx) continue;
+        if (ht[w] == NH_UNKNOWN) prefetch_pair(P, w, g, tab, s_q);
+        add(w);
+      }
+    }
+    for (uint32_t i = 0; i < nn; ++i) fr[i] = nx[i];
+    nf = nn;
+  }
+}
+
+// Walk the resolved codes toward g from cell u for at most `hops` cells; queue the first unresolved
+// pair (and the DAG past it). Returns the hops left when the walk reached g, else 0.
+__device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab,
+                                  uint32_t hops) {
+  for (uint32_t h = 0; h < hops; ++h) {
+    if (u == g) return hops - h;
+    const uint8_t cu = P.nh[(uint64_t)tab * P.nstride + u];
+    if (cu == NH_UNKNOWN || cu == NH_PENDING || cu == NH_PENDING_S) {
+      if (cu == NH_UNKNOWN) prefetch_pair(P, u, g, tab, s_q);
+      if (P.dag_prefetch) dag_prefetch(P, s_q, u, g, tab);
+      return 0;
+    }
+    if (cu >= NH_STAY) return 0;  // a stay code
+    u = step_cell(u, cu, P.W);
+  }
+  return 0;
+}
+
 // Parallel: the next hop of every agent from the cell its resolved code points at (the pair the
-// movement phase or the next step reads after the agent moves, tswap.rs:263-273); speculative,
-// bounded by half the queue like rules_prefetch.
+// movement phase or the next step reads after the agent moves, tswap.rs:263-273), walked `hops`
+// resolved cells ahead; speculative, bounded by half the queue like rules_prefetch.
+//  * an agent whose own code is still unresolved (just assigned, goal swapped) gets the DAG past its
+//    cell queued now, beside its needed pair, instead of one cell per step after each wait
+//    (prefetch_ext bit 0);
+//  * an agent heading to a pickup whose walk reaches it continues along the delivery leg: the
+//    state machine switches its goal there (tswap.rs:113-118) (prefetch_ext bit 1).
 __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x, hops = P.wide_prefetch ? P.wide_prefetch : 1u;
   for (uint32_t k = tid; k < P.n; k += bd) {
@@ -534,71 +609,29 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
     // heading to a pickup: the pair the state machine needs on arrival (goal := delivery,
     // tswap.rs:113-118) is known since the assignment — (arrival cell, delivery goal). The arrival
     // cell is the agent's current goal: rule-3/4 swaps may have traded the task's pickup cell away.
+    uint32_t pc = 0, dc = 0;
+    int32_t dtab = -1;
     if (P.mode != MODE_STEP && P.m > 0 && P.st[k] == ST_TO_PICKUP) {
       const int32_t tk = P.task[k];
       if (tk >= 0 && (uint32_t)tk < P.m) {
-        const uint32_t pc = S.G[k], dc = P.dlv[tk];
+        pc = S.G[k];
+        dc = P.dlv[tk];
         const int32_t dt = P.goal_tab[dc];
-        if (dt >= 0 && pc != dc && P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) prefetch_pair(P, pc, dc, dt, s_q);
+        if (dt >= 0 && pc != dc) {
+          dtab = dt;
+          if (P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) prefetch_pair(P, pc, dc, dt, s_q);
+        }
       }
     }
     const int32_t tab = S.GT[k];
     const uint8_t c = S.NHC[k];
-    if (tab < 0 || c >= NH_STAY || S.V[k] == S.G[k]) continue;
-    // walk the resolved codes up to `hops` cells ahead; queue the first unresolved one
-    uint32_t u = step_cell(S.V[k], c, P.W);
-    for (uint32_t h = 0; h < hops && u != S.G[k]; ++h) {
-      const uint8_t cu = P.nh[(uint64_t)tab * P.nstride + u];
-      if (cu == NH_UNKNOWN || cu == NH_PENDING || cu == NH_PENDING_S) {
-        if (cu == NH_UNKNOWN) prefetch_pair(P, u, S.G[k], tab, s_q);
-        // levels past it: whichever neighbour u's code picks lies one step closer to the goal
-        // (every get_path is a shortest path), so the shortest-path DAG ahead of u is where the
-        // agent goes next. Its cells are queued level by level (frontier capped at DAG_WIDTH; a
-        // resolved cell contributes only the cell its code points at), so the agent's path
-        // resolves several cells per A* latency instead of one.
-        if (P.dag_prefetch) {
-          constexpr uint32_t DAG_WIDTH = 4;
-          const uint16_t* dt = P.dist + (uint64_t)tab * P.nstride;
-          const uint8_t* ht = P.nh + (uint64_t)tab * P.nstride;
-          const uint32_t g = S.G[k];
-          uint32_t fr[DAG_WIDTH], nf = 1;
-          fr[0] = u;
-          for (uint32_t lv = 0; lv < P.dag_prefetch && nf > 0u; ++lv) {
-            uint32_t nx[DAG_WIDTH], nn = 0;
-            auto add = [&](uint32_t w) {
-              for (uint32_t i = 0; i < nn; ++i)
-                if (nx[i] == w) return;
-              if (nn < DAG_WIDTH) nx[nn++] = w;
-            };
-            for (uint32_t i = 0; i < nf; ++i) {
-              const uint32_t x = fr[i];
-              const uint8_t cx = ht[x];
-              if (cx < NH_STAY) {  // resolved: the agent's path continues at one cell
-                const uint32_t w = step_cell(x, cx, P.W);
-                if (w != g) add(w);
-                continue;
-              }
-              if (cx == NH_STAY) continue;
-              const uint32_t dx = dt[x];
-              const uint8_t nb = P.nbmask[x];
-#pragma unroll
-              for (uint32_t d = 0; d < 4u; ++d) {
-                if (!((nb >> d) & 1u)) continue;
-                const uint32_t w = step_cell(x, d, P.W);
-                if (w == g || (uint32_t)dt[w] + 1u != dx) continue;
-                if (ht[w] == NH_UNKNOWN) prefetch_pair(P, w, g, tab, s_q);
-                add(w);
-              }
-            }
-            for (uint32_t i = 0; i < nn; ++i) fr[i] = nx[i];
-            nf = nn;
-          }
-        }
-        break;
-      }
-      if (cu >= NH_STAY) break;  // a stay code
-      u = step_cell(u, cu, P.W);
+    if (tab < 0 || S.V[k] == S.G[k] || c == NH_STAY) continue;
+    if (c > NH_STAY) {  // own pair unresolved (queued as needed by the refresh)
+      if ((P.prefetch_ext & 1u) && P.dag_prefetch) dag_prefetch(P, s_q, S.V[k], S.G[k], tab);
+      continue;
     }
+    const uint32_t left = walk_prefetch(P, s_q, step_cell(S.V[k], c, P.W), S.G[k], tab, hops);
+    if (left > 0u && dtab >= 0 && (P.prefetch_ext & 2u)) walk_prefetch(P, s_q, pc, dc, dtab, left);
   }
   __syncthreads();
 }
