@@ -19,10 +19,15 @@
 //    fixed mask (CB_EVEN) inside every block.
 //  * LDS: the free-cell blocks FR (shared by the workgroup's waves); per wave the visited
 //    blocks V, two interleaved dedup flag bitmaps and two active-block lists. Goals in
-//    flight per CU are bounded by LDS and the level loop is latency-bound, so the west-step
-//    blocks WL (bit set = the west neighbour was reached one level earlier; written once per
-//    activation, read only by the decode) live in per-wave global scratch, updated with
-//    fire-and-forget 64-bit workgroup-scope atomic ORs (performed in L2).
+//    flight per CU are bounded by LDS and the level loop is issue-bound, so by default the
+//    west-step blocks WL (bit set = the west neighbour was reached one level earlier; written
+//    once per activation, read only by the decode) live in per-wave global scratch, updated
+//    with fire-and-forget 64-bit workgroup-scope atomic ORs. Measured cost (den520d, 10k goals,
+//    PMC): the scratch of 384 waves per XCD outgrows the XCD's L2 and its lines are written
+//    back ~18x per goal — 1.64 GB of WRITE_SIZE per launch on top of 1.31 GB of tables.
+//    k_bfs_blk<true> (TSW_BFS_WLS=1) keeps WL in LDS instead (plain owner-exclusive RMW):
+//    traffic 1.03x the algorithmic bytes and 15 % fewer cycles per goal, but 6 instead of 12
+//    goals in flight per CU — 3.21 vs 2.71 ms per launch, so the default stays global.
 //  * Level lvl processes exactly the blocks that gain cells at distance lvl:
 //    new = expand(V & parity(lvl-1)) & FR & ~V (race-free inside the wave: the 4-grid is
 //    bipartite, so bits written during a level are never sources in the same level).
@@ -95,15 +100,18 @@ __device__ __forceinline__ uint32_t ct_slot(uint32_t lane, uint32_t j) {
 
 // LDS dwords of one wave; must match the carve in k_bfs_blk: V (nbp rounded to even u64), flags,
 // then the list / run-table / staging region LS, 16-B aligned (every part is a multiple of 4 dwords).
-__host__ __device__ __forceinline__ uint32_t blk_bfs_words(uint32_t nbp, uint32_t nfk, uint32_t cap) {
+__host__ __device__ __forceinline__ uint32_t blk_bfs_words(uint32_t nbp, uint32_t nfk, uint32_t cap, bool wls) {
   const uint32_t ls = 2u * cap < CT_U16 ? CT_U16 : 2u * cap;  // u16 entries: two lists, run table, staging
-  return 2u * ((nbp + 1u) & ~1u) + 2u * nfk + ((ls + 7u) >> 3) * 4u;
+  return (wls ? 4u : 2u) * ((nbp + 1u) & ~1u) + 2u * nfk + ((ls + 7u) >> 3) * 4u;
 }
 // u64 words of the workgroup's shared part (FR u64 + AB u32), rounded to 16 B
 __host__ __device__ __forceinline__ uint32_t blk_shared_u64(uint32_t nbp) {
   return (nbp + (nbp + 1u) / 2u + 1u) & ~1u;
 }
 
+// WLS: the west-step blocks WL live in the wave's LDS (after V) instead of global scratch — no
+// memory-side atomics, at the cost of ~nbp*8 more LDS bytes per goal in flight.
+template <bool WLS>
 __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   extern __shared__ __align__(16) uint64_t smem64[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
@@ -112,11 +120,16 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   uint64_t* FRs = smem64;
   uint32_t* AB = reinterpret_cast<uint32_t*>(smem64 + nbp);  // [nbp] first run-start index of block p
   uint64_t* V;
+  uint64_t* WLl = nullptr;  // WLS: the LDS west-step blocks
   uint32_t* FL;  // 2 * nfk interleaved flag dwords: block t -> dword t & kmask, bit t >> klog
   uint16_t* LS;  // 2 * cap list entries / decode run table
   {
-    uint32_t* b = reinterpret_cast<uint32_t*>(smem64 + blk_shared_u64(nbp)) + wv * blk_bfs_words(nbp, nfk, cap);
+    uint32_t* b = reinterpret_cast<uint32_t*>(smem64 + blk_shared_u64(nbp)) + wv * blk_bfs_words(nbp, nfk, cap, WLS);
     V = reinterpret_cast<uint64_t*>(b);
+    if constexpr (WLS) {
+      WLl = V + ((nbp + 1u) & ~1u);
+      b += 2u * ((nbp + 1u) & ~1u);
+    }
     FL = b + 2u * ((nbp + 1u) & ~1u);
     LS = reinterpret_cast<uint16_t*>(FL + 2u * nfk);
   }
@@ -129,7 +142,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   const uint32_t gw = blockIdx.x * nwv + wv;
   uint16_t* anch = A.anch + (uint64_t)gw * A.nrs;  // compact anchors (run-start index)
   uint16_t* lovf = A.lovf + (uint64_t)gw * 2u * nbp;
-  unsigned long long* WL = A.wlg + (uint64_t)gw * nbp;
+  unsigned long long* WL = WLS ? reinterpret_cast<unsigned long long*>(WLl) : A.wlg + (uint64_t)gw * nbp;
   const uint32_t idle_p = Bp + BW;  // guard block of block row 0: FR = 0, all neighbours in range
   uint64_t t_bfs = 0, t_dec = 0, n_lvl = 0, n_chunk = 0;
 
@@ -202,7 +215,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       const uint32_t bx = p - __umulhi(p, A.bp_magic) * Bp;
       const uint64_t wf = ((f0 << 1) & ~COL0) | ((bx & 3u) ? ((fw >> 7) & COL0) : 0ull);
       const uint64_t rs = f0 & ~wf;
-      uint64_t rsn = nw & rs;
+      uint64_t rsn = (A.dbg & 4u) ? 0ull : nw & rs;
       while (rsn) {
         const uint32_t bb = (uint32_t)__builtin_ctzll(rsn);
         anch[AB[p] + (uint32_t)__popcll(rs & ((1ull << bb) - 1ull))] = (uint16_t)lvl;
@@ -228,7 +241,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       const uint32_t wf = ((f0 << 1) & ~C0) | ((bx & 3u) ? ((fw >> 7) & C0) : 0u);
       const uint32_t rs = f0 & ~wf;
       const uint32_t below = __popc(partner(rs));  // the low half's run starts precede ours
-      uint32_t rsn = nw & rs;
+      uint32_t rsn = (A.dbg & 4u) ? 0u : nw & rs;
       const uint32_t base = AB[p] + (h ? below : 0u);
       while (rsn) {
         const uint32_t bb = (uint32_t)__builtin_ctz(rsn);
@@ -330,7 +343,10 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         // zero guard block
         V[p] = vv;
         const uint64_t wln = nw & (((v0 << 1) & ~COL0) | ((vw >> 7) & COL0));
-        if (wln) wl_or(WL + p, (unsigned long long)wln);
+        if (wln && !(A.dbg & 2u)) {
+          if constexpr (WLS) WL[p] |= wln;  // owner-exclusive within the level, program order across levels
+          else wl_or(WL + p, (unsigned long long)wln);
+        }
         bad |= act && nw == 0ull;  // entries must gain a cell
         anchors(p, nw, f0, fw, lvl);
         push(p, nw, vv, f0, fw, fe, fn, fs, vw, ve, vn, vs, Fn, Ln, On);
@@ -352,7 +368,10 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         const uint32_t vv = v0 | nw;
         V32[o] = vv;  // owner-exclusive (deduplicated list, one lane per half); idle lanes rewrite 0
         const uint32_t wln = nw & (((v0 << 1) & ~C0) | ((vw >> 7) & C0));
-        if (wln) wl_or32(WL32 + o, wln);
+        if (wln && !(A.dbg & 2u)) {
+          if constexpr (WLS) WL32[o] |= wln;
+          else wl_or32(WL32 + o, wln);
+        }
         const uint32_t nwp = partner(nw);
         bad |= act && (nw | nwp) == 0u;  // entries must gain a cell
         anchors2(p, nw, f0, fw, lvl);
@@ -398,7 +417,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
     // is u16). Bit b belongs to run popc(rsw & bits<=b) - 1 (<= 16 runs per word); C goes to row
     // popc(...) of this lane's column of the run table.
     const uint8_t* V8 = reinterpret_cast<const uint8_t*>(V);
-    const uint8_t* WL8 = reinterpret_cast<const uint8_t*>(WL);  // global, L2-resident
+    const uint8_t* WL8 = reinterpret_cast<const uint8_t*>(WL);  // LDS (WLS) or global, L2-resident
     const uint8_t* FR8 = reinterpret_cast<const uint8_t*>(FRs);
     uint16_t* D = A.dist + slot * A.dstride;
     const uint32_t Ww = (W + 31u) >> 5, nwords = A.H * Ww;
@@ -429,7 +448,8 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         if (4u * o.cw + j < BW) {
           const uint32_t off = (o.p0 + j) * 8u + o.r;
           o.vis |= (uint32_t)V8[off] << (8u * j);
-          o.wl |= (uint32_t)__builtin_nontemporal_load(WL8 + off) << (8u * j);
+          if constexpr (WLS) o.wl |= (uint32_t)WL8[off] << (8u * j);
+          else o.wl |= (uint32_t)__builtin_nontemporal_load(WL8 + off) << (8u * j);
           o.f0 |= (uint32_t)FR8[off] << (8u * j);
         }
       }
@@ -534,7 +554,14 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         for (uint32_t q = lane; q < nch; q += 64u) {
           const uint32_t c0 = base + 8u * q;
           if (c0 >= cs && c0 + 8u <= ce) {
-            *reinterpret_cast<uint4*>(D + c0) = *reinterpret_cast<const uint4*>(LS + 8u * q);
+            const uint4 v4 = *reinterpret_cast<const uint4*>(LS + 8u * q);
+            if (A.dbg & 1u) {
+              typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+              const u32x4 vv = {v4.x, v4.y, v4.z, v4.w};
+              __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(D + c0));
+            } else {
+              *reinterpret_cast<uint4*>(D + c0) = v4;
+            }
           } else {
 #pragma unroll
             for (uint32_t b = 0; b < 8u; ++b)
@@ -591,8 +618,8 @@ uint32_t bfs_blk_klog(uint32_t nbp) {
   return kl;
 }
 
-uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds) {
-  const size_t per_wave = (size_t)blk_bfs_words(nbp, 1u << bfs_blk_klog(nbp), cap) * 4u;
+uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds, bool wls) {
+  const size_t per_wave = (size_t)blk_bfs_words(nbp, 1u << bfs_blk_klog(nbp), cap, wls) * 4u;
   const size_t shared = (size_t)blk_shared_u64(nbp) * 8u;  // FR u64 + AB u32
   if (max_lds <= 0 || shared + per_wave > (size_t)max_lds) return 0;
   return (uint32_t)std::min<size_t>(16u, ((size_t)max_lds - shared) / per_wave);
@@ -603,16 +630,19 @@ hipError_t launch_bfs_blk(const BlkBfsArgs& A0, int max_lds, int num_cu, hipStre
   BlkBfsArgs A = A0;
   A.klog = bfs_blk_klog(A.nbp);
   A.bp_magic = (uint32_t)((0xFFFFFFFFull + A.Bp) / A.Bp);  // ceil(2^32 / Bp): exact p / Bp for p*Bp < 2^32
-  const size_t per_wave = (size_t)blk_bfs_words(A.nbp, 1u << A.klog, A.cap) * 4u;
+  const bool wls = A.wls != 0u;
+  const size_t per_wave = (size_t)blk_bfs_words(A.nbp, 1u << A.klog, A.cap, wls) * 4u;
   const size_t shared = (size_t)blk_shared_u64(A.nbp) * 8u;  // FR u64 + AB u32
-  const uint32_t nwv = std::min<uint32_t>(A.max_waves, bfs_blk_waves_per_block(A.nbp, A.cap, max_lds));
+  const uint32_t nwv = std::min<uint32_t>(A.max_waves, bfs_blk_waves_per_block(A.nbp, A.cap, max_lds, wls));
   if (nwv == 0 || A.nbp > 0x10000u || A.cap > 0x8000u) return hipErrorInvalidValue;
   const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cu, (A.k + nwv - 1u) / nwv));
   if ((uint64_t)grid * nwv > A.scratch_waves) return hipErrorInvalidValue;
   const size_t lds = shared + nwv * per_wave;
-  hipError_t e = hipFuncSetAttribute((const void*)k_bfs_blk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const void* fn = wls ? (const void*)k_bfs_blk<true> : (const void*)k_bfs_blk<false>;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_bfs_blk, dim3(grid), dim3(nwv * 64u), lds, s, A);
+  if (wls) hipLaunchKernelGGL(k_bfs_blk<true>, dim3(grid), dim3(nwv * 64u), lds, s, A);
+  else hipLaunchKernelGGL(k_bfs_blk<false>, dim3(grid), dim3(nwv * 64u), lds, s, A);
   return hipGetLastError();
 }
 

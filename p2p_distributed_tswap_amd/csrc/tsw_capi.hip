@@ -55,6 +55,8 @@ struct Tunables {
   bool bfs_order = true;          // TSW_BFS_ORDER=0: keep the caller's goal order (no LPT)
   bool bfs_prof = false;          // TSW_BFS_PROF: print K1 cycle split per launch
   bool bfs_nostage = false;       // TSW_BFS_NOSTAGE: k_bfs_blk writes rows lane-strided (no LDS staging)
+  uint32_t bfs_dbg = 0;           // TSW_BFS_DBG: k_bfs_blk diagnostics (BlkBfsArgs::dbg)
+  uint32_t bfs_wls = 0;           // TSW_BFS_WLS: k_bfs_blk west-step blocks in LDS
   uint32_t wave_hcap = 0;         // TSW_ASTAR_WAVE_HCAP: k_astar_wave LDS heap entries (0 = default)
   int astar_global_gs = -1;       // TSW_ASTAR_GLOBAL_GS: -1 auto, 0 LDS g-scores, 1 global slots
   bool astar_tier2 = true;        // TSW_ASTAR_NO_TIER2: skip the LDS-heap/global-g second tier
@@ -86,6 +88,8 @@ struct Tunables {
     t.bfs_order = num("TSW_BFS_ORDER", 0, 1, 1) != 0;
     t.bfs_prof = getenv("TSW_BFS_PROF") != nullptr;
     t.bfs_nostage = getenv("TSW_BFS_NOSTAGE") != nullptr;
+    t.bfs_dbg = (uint32_t)num("TSW_BFS_DBG", 0, 7, 0);
+    t.bfs_wls = (uint32_t)num("TSW_BFS_WLS", 0, 1, t.bfs_wls);
     t.wave_hcap = (uint32_t)num("TSW_ASTAR_WAVE_HCAP", 4, 1 << 20, 0);
     t.astar_global_gs = (int)num("TSW_ASTAR_GLOBAL_GS", 0, 1, -1);
     t.astar_tier2 = getenv("TSW_ASTAR_NO_TIER2") == nullptr;
@@ -605,7 +609,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   const uint32_t bfs_mode = c->tun.bfs_mode;
   uint32_t nbw = 0;
   if ((bfs_mode == 0 || bfs_mode == 3) && c->nbp <= 0x10000u)
-    nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->tun.blk_cap, c->max_lds));
+    nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->tun.blk_cap, c->max_lds, c->tun.bfs_wls != 0u));
   if (nbw == 0 && bfs_mode == 3) RET(TSW_EINVAL, "k_bfs_blk does not fit this grid (TSW_BFS_KERNEL=blk)");
   if (nbw > 0) {
     Timer t(c, CAT_BFS);
@@ -641,6 +645,8 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     A.err = &c->d_stat->err;
     A.vec16 = vec16 ? 1u : 0u;
     A.stage = (dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u && !c->tun.bfs_nostage) ? 1u : 0u;
+    A.dbg = c->tun.bfs_dbg;
+    A.wls = c->tun.bfs_wls;
     A.max_waves = nbw;
     A.scratch_waves = std::min(c->wave_scratch, c->wlg_waves);
     A.prof = (uint64_t*)bfs_prof_buf(c);

@@ -61,8 +61,10 @@ struct BlkBfsArgs {
   uint32_t max_waves;
   uint64_t scratch_waves;
   uint64_t* prof;         // optional: [bfs cycles, decode cycles, levels, chunks] summed over waves
+  uint32_t dbg;           // TSW_BFS_DBG (diagnostics): 1 nontemporal table stores, 2 no WL atomics, 4 no anchors
+  uint32_t wls;           // west-step blocks in LDS (k_bfs_blk<true>) instead of global scratch
 };
-uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds);
+uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds, bool wls);
 hipError_t launch_bfs_blk(const BlkBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
 
 // K1 v4 (tsw_bfs_big.hip): one WORKGROUP per goal over 8x8 cell blocks, free blocks and run

@@ -73,6 +73,13 @@ def test_bfs_kernels_bit_exact(kernel, name):
     _check(rows, _goals(rows, 40, 7), TSW_BFS_KERNEL=kernel)
 
 
+@pytest.mark.parametrize("name", sorted(GRIDS))
+def test_bfs_blk_lds_west_steps(name):
+    """k_bfs_blk with the west-step blocks in LDS (TSW_BFS_WLS=1: no global scratch atomics)."""
+    rows = GRIDS[name]()
+    _check(rows, _goals(rows, 40, 9), TSW_BFS_KERNEL="blk", TSW_BFS_WLS=1)
+
+
 @pytest.mark.parametrize("cap", [1, 3, 17])
 def test_bfs_wave_list_overflow(cap):
     """Lists longer than the LDS capacity spill to the per-wave global overflow area."""
@@ -80,10 +87,11 @@ def test_bfs_wave_list_overflow(cap):
     _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="wave", TSW_BFS_LISTCAP=cap)
 
 
+@pytest.mark.parametrize("wls", [0, 1])
 @pytest.mark.parametrize("cap", [1, 3, 17])
-def test_bfs_blk_list_overflow(cap):
+def test_bfs_blk_list_overflow(cap, wls):
     rows = maps.cave_map(128, 97, 9)
-    _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="blk", TSW_BFS_BLKCAP=cap)
+    _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="blk", TSW_BFS_BLKCAP=cap, TSW_BFS_WLS=wls)
 
 
 @pytest.mark.parametrize("kernel", ["blk", "wave", "big"])
