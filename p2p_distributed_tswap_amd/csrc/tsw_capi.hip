@@ -67,6 +67,7 @@ struct Tunables {
   uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
   uint32_t prefetch_ext = 7;      // TSW_PREFETCH_EXT: bit 0 DAG from an agent's own unresolved cell, bit 1 walk past the pickup, bit 2 walk-ahead for agents a firing changed (C3 476 -> 409 ms with bits 0-1)
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
+  bool plan_ap = true;            // TSW_PLAN_AP=0: no partial agent arrays in LDS (k_plan AP) when all do not fit
   uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
@@ -100,6 +101,7 @@ struct Tunables {
     t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 16, t.dag_prefetch);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
+    t.plan_ap = num("TSW_PLAN_AP", 0, 1, 1) != 0;
     t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
@@ -990,10 +992,13 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
   // without the agent arrays, the rules relabel's pointer-doubling buffers come next
-  bool fl = !ag && c->tun.flinks_lds && plan_lds_bytes(n, P.ncell, m, false, false, false, true) <= budget;
-  bool oc = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl) <= budget;
-  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl) <= budget;
+  // else the arrays every round touches (k_plan AP), else the pointer-doubling buffers
+  bool ap = !ag && c->tun.plan_ap && plan_lds_bytes(n, P.ncell, m, false, false, false, false, true) <= budget;
+  bool fl = !ag && !ap && c->tun.flinks_lds && plan_lds_bytes(n, P.ncell, m, false, false, false, true) <= budget;
+  bool oc = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, ap) <= budget;
+  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl, ap) <= budget;
   P.f_lds = fl;
+  P.agents_part = ap;
   P.agents_lds = ag;
   P.occ_lds = oc;
   P.tasks_lds = tk;
@@ -1021,7 +1026,7 @@ int build_occ(tsw_ctx* c, uint32_t n) {
 int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   *c->h_ctl = init;
   HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
-  size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds);
+  size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds, P.agents_part);
   // coop mode: the planner block reserves its CU's whole LDS so no worker wave is placed beside it
   // (they would compete for its SIMDs and LDS bandwidth on the critical path)
   if (P.coop) lds = std::max<size_t>(lds, (size_t)std::max(c->max_lds - 2048, 0));
@@ -1149,8 +1154,10 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       c->st.rule_rounds += k.rule_rounds;
       c->st.move_rounds += k.move_rounds;
       if (c->tun.plan_debug) {
-        unsigned long long tk[24];
+        unsigned long long tk[32];
         HIPCHK(hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[k_plan] PRE1 publish us %.0f (%llu) | rules init us %.0f prefetch us %.0f publish us %.0f (%llu)\n",
+                tk[24] / 100.0, tk[25], tk[26] / 100.0, tk[27] / 100.0, tk[28] / 100.0, tk[29]);
         fprintf(stderr, "[k_plan] wave rules kcycles: load %.0f stale %.0f fast %.0f update %.0f slow %.0f rot %.0f | "
                 "loads %llu fast firings %llu\n", tk[16] / 1e3, tk[17] / 1e3, tk[18] / 1e3, tk[19] / 1e3, tk[20] / 1e3,
                 tk[21] / 1e3, tk[22], tk[23]);
@@ -1447,8 +1454,8 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned status", e);
   if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
-  if ((e = hipMalloc(&c->d_ticks, 24 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
-  if ((e = hipMemsetAsync(c->d_ticks, 0, 24 * sizeof(unsigned long long), c->s)) != hipSuccess)
+  if ((e = hipMalloc(&c->d_ticks, 32 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
+  if ((e = hipMemsetAsync(c->d_ticks, 0, 32 * sizeof(unsigned long long), c->s)) != hipSuccess)
     return fail("memset ticks", e);
   hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, c->device);
   if (c->wall_khz <= 0) c->wall_khz = 100000;
@@ -1922,7 +1929,7 @@ int tsw_reset_stats(tsw_ctx* c) {
   const uint64_t tabs = c->st.tables;
   c->st = tsw_stats{};
   c->st.tables = tabs;
-  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 24 * sizeof(unsigned long long), c->s);
+  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 32 * sizeof(unsigned long long), c->s);
   return TSW_OK;
 }
 

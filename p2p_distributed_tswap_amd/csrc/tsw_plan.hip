@@ -697,14 +697,16 @@ __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
     }                                                \
   } while (0)
 
-template <bool AG, bool OC>
+// AG: every agent array in LDS. AP (AG false, n too large for AG): the arrays every rules round and
+// movement pass touches — V, G, SUCC, NHC, ONC, CANDC — in LDS, the rest (GT, DEC, MK, F1/F2) global.
+template <bool AG, bool OC, bool AP>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
   __shared__ uint32_t s_q[3], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
-  __shared__ unsigned long long s_tick[24], s_tlast, s_tp;
+  __shared__ unsigned long long s_tick[32], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
   __shared__ uint32_t s_nassign, s_npick;  // diagnostics: this step's assignments / pickup arrivals
   const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6, nwaves = bd >> 6;
@@ -731,6 +733,18 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     S.DEC = carve(n);
     S.ONC = carve(n);
     S.CANDC = carve(n);
+  } else if constexpr (AP) {
+    S.V = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
+    S.G = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
+    S.SUCC = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
+    S.NHC = carve(n);
+    S.ONC = carve(n);
+    S.CANDC = carve(n);
+    S.GT = P.gt;
+    S.F1 = P.f1;
+    S.F2 = P.f2;
+    S.DEC = P.dec;
+    S.MK = P.mk;
   } else {
     S.V = P.v;
     S.G = P.g;
@@ -775,6 +789,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       S.V[k] = P.v[k];
       S.G[k] = g;
       S.DEC[k] = P.dec[k];
+    } else if constexpr (AP) {
+      S.V[k] = P.v[k];
+      S.G[k] = g;
     }
     S.GT[k] = P.goal_tab[g];
     S.NHC[k] = NHC_DIRTY;
@@ -791,7 +808,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     s_q[1] = 0;  // speculative queue (coop mode)
     s_q[2] = 0;  // publishes (coop mode)
-    for (int k = 0; k < 24; ++k) s_tick[k] = 0;
+    for (int k = 0; k < 32; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
     // coop mode: tell the host the planner is resident, so the workers it launches next cannot
@@ -932,7 +949,14 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // step start: queue every agent's next hop from the cell it is about to enter now, so
       // the assignment exit's K3 batch (if any) already carries what the movement phase reads
       if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, s_q);
-      if (P.coop && tid == 0) coop_publish(P, s_q);  // speculative pairs start resolving now
+      if (P.coop && tid == 0) {  // speculative pairs start resolving now
+        const unsigned long long t0 = P.dbg ? wall_clock64() : 0ull;
+        coop_publish(P, s_q);
+        if (P.dbg) {
+          s_tick[24] += wall_clock64() - t0;
+          s_tick[25] += 1;
+        }
+      }
       // diagnostics: PRE1 waits by timestep bucket (t < 50, < 150, < 400, < 1000, later)
       const uint32_t tt = s_ctl.t;
       const uint32_t wkind = sec == SEC_PRE1 ? (tt < 50 ? 1u : tt < 150 ? 2u : tt < 400 ? 3u : tt < 1000 ? 4u : 5u) : 0u;
@@ -961,8 +985,24 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       if (P.dbg && tid == 0) s_tp = wall_clock64();
       rules_init(P, S);
       if (tid == 0) s_ctl.relabel_full += 1;
+      if (P.dbg && tid == 0) {
+        const unsigned long long nw = wall_clock64();
+        s_tick[26] += nw - s_tp;
+        s_tp = nw;
+      }
       if (P.prefetch) rules_prefetch(P, S, s_q);
-      if (P.coop && tid == 0) coop_publish(P, s_q);
+      if (P.dbg && tid == 0) {
+        const unsigned long long nw = wall_clock64();
+        s_tick[27] += nw - s_tp;
+        s_tp = nw;
+      }
+      if (P.coop && tid == 0) {
+        coop_publish(P, s_q);
+        if (P.dbg) {
+          s_tick[28] += wall_clock64() - s_tp;
+          s_tick[29] += 1;
+        }
+      }
       if (tid == 0) s_cnt = 0;
       PLAN_TICK(15);
       // One firing agent per round (tswap.rs:180-252 in agent order): fire(b) applies b's rule 3
@@ -1774,6 +1814,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       P.g[k] = S.G[k];
       P.dec[k] = S.DEC[k];
     }
+  if constexpr (AP)
+    for (uint32_t k = tid; k < n; k += bd) {
+      P.v[k] = S.V[k];
+      P.g[k] = S.G[k];
+    }
   if constexpr (OC)
     for (uint32_t c = tid; c < P.ncell; c += bd) P.occ[c] = S.OCC[c];
   if (tid == 0) {
@@ -1787,7 +1832,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     P.ctl->err |= err;
     s_tick[s_tsec] += wall_clock64() - s_tlast;
     if (P.sec_ticks)
-      for (int k = 0; k < 24; ++k) P.sec_ticks[k] += s_tick[k];
+      for (int k = 0; k < 32; ++k) P.sec_ticks[k] += s_tick[k];
   }
 }
 
@@ -1814,10 +1859,12 @@ __global__ void k_occ_flag(uint32_t* occ, const uint32_t* cnt, uint32_t ncell, u
   }
 }
 
-size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks, bool flinks) {
+size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks, bool flinks,
+                      bool partial) {
   auto r16 = [](size_t b) { return (b + 15u) & ~(size_t)15u; };
   size_t b = r16(1024 * 4);
   if (agents) b += 4 * r16((size_t)n * 4) + 3 * r16((size_t)(n + 1) * 4) + 4 * r16(n);
+  else if (partial) b += 3 * r16((size_t)n * 4) + 3 * r16(n);
   else if (flinks) b += 2 * r16((size_t)(n + 1) * 4);
   if (occ) b += r16((size_t)ncell * 4) + r16((size_t)ncell * 8);
   if (tasks) b += r16((size_t)m * 4) + r16(m);
@@ -1832,20 +1879,22 @@ hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cn
   return hipGetLastError();
 }
 
-template <bool AG, bool OC>
+template <bool AG, bool OC, bool AP>
 static hipError_t launch_plan_t(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s) {
-  hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC, AP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_plan<AG, OC>), dim3(1), dim3(block), lds, s, P);
+  hipLaunchKernelGGL((k_plan<AG, OC, AP>), dim3(1), dim3(block), lds, s, P);
   return hipGetLastError();
 }
 
 hipError_t launch_plan(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s) {
-  if (P.agents_lds && P.occ_lds) return launch_plan_t<true, true>(P, lds, block, s);
-  if (P.agents_lds) return launch_plan_t<true, false>(P, lds, block, s);
-  if (P.occ_lds) return launch_plan_t<false, true>(P, lds, block, s);
-  return launch_plan_t<false, false>(P, lds, block, s);
+  if (P.agents_lds && P.occ_lds) return launch_plan_t<true, true, false>(P, lds, block, s);
+  if (P.agents_lds) return launch_plan_t<true, false, false>(P, lds, block, s);
+  if (P.agents_part && P.occ_lds) return launch_plan_t<false, true, true>(P, lds, block, s);
+  if (P.agents_part) return launch_plan_t<false, false, true>(P, lds, block, s);
+  if (P.occ_lds) return launch_plan_t<false, true, false>(P, lds, block, s);
+  return launch_plan_t<false, false, false>(P, lds, block, s);
 }
 
 }  // namespace tsw
