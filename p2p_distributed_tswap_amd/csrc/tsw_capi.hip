@@ -67,7 +67,10 @@ struct Tunables {
   uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
   uint32_t prefetch_ext = 7;      // TSW_PREFETCH_EXT: bit 0 DAG from an agent's own unresolved cell, bit 1 walk past the pickup, bit 2 walk-ahead for agents a firing changed (C3 476 -> 409 ms with bits 0-1)
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
-  bool plan_ap = true;            // TSW_PLAN_AP=0: no partial agent arrays in LDS (k_plan AP) when all do not fit
+  // TSW_PLAN_AP=1: partial agent arrays in LDS (k_plan AP) when all do not fit. Off: on the full wh10k
+  // plan its rules rounds were 20 % faster (fire 3.27 -> 2.60 s) but movement pass 1 took 5.3 s
+  // instead of 0.25 s late in the plan (18.3 vs 13.8 s end to end), not yet explained
+  bool plan_ap = false;
   uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
@@ -101,7 +104,7 @@ struct Tunables {
     t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 16, t.dag_prefetch);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
-    t.plan_ap = num("TSW_PLAN_AP", 0, 1, 1) != 0;
+    t.plan_ap = num("TSW_PLAN_AP", 0, 1, 0) != 0;
     t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
