@@ -75,6 +75,7 @@ struct Tunables {
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
   bool task_chains = true;        // TSW_TASK_CHAINS=0: no task-chain jobs for the coop workers
+  bool chain_preempt = true;      // TSW_CHAIN_PREEMPT=0: chain workers finish a chain before serving queued pairs
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
 
   static Tunables from_env() {
@@ -109,6 +110,7 @@ struct Tunables {
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
     t.task_chains = num("TSW_TASK_CHAINS", 0, 1, 1) != 0;
+    t.chain_preempt = num("TSW_CHAIN_PREEMPT", 0, 1, 1) != 0;
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
     return t;
   }
@@ -1051,6 +1053,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     // task chains take half the workers at most (a quarter with many agents: their needed bursts
     // are larger), the rest stay free for the pairs the planner waits on
     W.tmask = P.n > 2000u ? 3u : 1u;
+    W.preempt = c->tun.chain_preempt ? 1u : 0u;
     W.hflags = c->d_flags;
     W.gs_all = c->d_gs;
     W.epochs = c->d_epochs;
@@ -1174,6 +1177,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                   "MOVE %u/%u | PRE1 never queued: assigned %u, picked up %u | chain queries %llu of %llu\n", cc.dbg_need[0], cc.dbg_need[1], cc.dbg_need[2],
                   cc.dbg_need[3], cc.dbg_need[4], cc.dbg_need[5], cc.dbg_need[6], cc.dbg_need[7],
                   (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
+          fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u\n",
+                  cc.waits ? (double)cc.dbg_depth / cc.waits : 0.0, cc.dbg_depth_max);
           fprintf(stderr, "[k_plan] worker A* ms (queries): needed %.1f (%u) spec %.1f (%u) task chains %.1f (%u)\n",
                   cc.wbusy[0] / (double)c->wall_khz, cc.wcount[0], cc.wbusy[1] / (double)c->wall_khz, cc.wcount[1],
                   cc.wbusy[2] / (double)c->wall_khz, cc.wcount[2]);

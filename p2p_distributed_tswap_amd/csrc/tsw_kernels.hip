@@ -1289,6 +1289,31 @@ __device__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint3
   }
 }
 
+// lane 0, non-blocking: claim one pair of the needed or the speculative queue (0 / 1), else -1.
+// A worker walking a task chain calls this between hops, so chains (lowest priority, up to ~100
+// A* each) never hold a worker while pairs the planner needs or will need soon are queued.
+__device__ int worker_try_claim(CoopCtl* cc, uint32_t* idx) {
+  for (;;) {
+    const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
+    if (cn < hn) {
+      if (w_cas(&cc->claim_n, cn, cn + 1u)) {
+        *idx = cn;
+        return 0;
+      }
+      continue;
+    }
+    const uint32_t hs = w_ld(&cc->head_s), cs = w_ld(&cc->claim_s);
+    if (cs < hs) {
+      if (w_cas(&cc->claim_s, cs, cs + 1u)) {
+        *idx = cs;
+        return 1;
+      }
+      continue;
+    }
+    return -1;
+  }
+}
+
 // global g-score slot tag (k_astar / tier-2 scheme: tag:10 | label:2 | g:20, cleared every 1023)
 __device__ __forceinline__ uint32_t slot_tag(uint32_t* GS, uint32_t ncell, uint32_t& ep, uint32_t lane) {
   if (ep % 1023u == 0u && ep > 0u) {
@@ -1407,6 +1432,21 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
     for (uint32_t hop = 0; hop < ncell && c != goal; ++hop) {
       // the planner is done: abandon the rest of the chain (nothing is marked pending)
       if ((uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? w_ld(&A.cc->stop) : 0u)) break;
+      // pairs the planner queued meanwhile come first (A.preempt)
+      while (A.preempt) {
+        int w2 = -1;
+        uint32_t i2 = 0;
+        if (lane == 0) w2 = worker_try_claim(A.cc, &i2);
+        w2 = __builtin_amdgcn_readfirstlane(w2);
+        if (w2 < 0) break;
+        i2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i2);
+        const uint32_t* e2 = reinterpret_cast<const uint32_t*>((w2 == 0 ? A.QN : A.QS) + i2);
+        const uint32_t v2 = w_ld(e2), g2 = w_ld(e2 + 1);
+        const int32_t t2 = (int32_t)w_ld(e2 + 2);
+        cur_q = (uint32_t)w2;
+        publish_code(v2, t2, resolve(v2, g2), false);
+        cur_q = 2u;
+      }
       uint8_t code = (uint8_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(c, tab) : 0u);
       if (code == NH_UNKNOWN) {
         code = resolve(c, goal);

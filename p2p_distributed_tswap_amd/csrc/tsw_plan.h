@@ -116,6 +116,7 @@ struct WorkerArgs {
   uint32_t gs_lds;    // 0: u32 g-scores in the global slots, 1: u32 in LDS, 2: bytes in LDS
   uint32_t stage_fb;  // free-cell bitmap staged in LDS (else read from global memory / L2)
   uint32_t tmask;     // workers with (blockIdx & tmask) == tmask also take task-chain jobs
+  uint32_t preempt;   // chain workers serve queued needed / speculative pairs between hops
   const uint32_t* hflags;  // host watchdog words (hflags[1] = abort)
   uint32_t* gs_all;   // per-wave global g-score slots (tier 2 / tier 3), ncell u32 each
   uint32_t* epochs;   // per-slot tag epochs

@@ -381,6 +381,12 @@ __device__ int coop_wait(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint
   if (tid == 0) {
     coop_publish(P, s_q);
     *s_flag = COOP_OK;
+    if (P.dbg) {
+      const uint32_t hs = min(s_q[1], P.qscap), cs = ld_agent(&P.cc->claim_s);
+      const uint32_t dep = hs > cs ? hs - cs : 0u;
+      P.cc->dbg_depth += dep;
+      P.cc->dbg_depth_max = max(P.cc->dbg_depth_max, dep);
+    }
   }
   __syncthreads();
   const unsigned long long t0 = wall_clock64();
