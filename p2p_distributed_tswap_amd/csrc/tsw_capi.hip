@@ -67,10 +67,7 @@ struct Tunables {
   uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
   uint32_t prefetch_ext = 7;      // TSW_PREFETCH_EXT: bit 0 DAG from an agent's own unresolved cell, bit 1 walk past the pickup, bit 2 walk-ahead for agents a firing changed (C3 476 -> 409 ms with bits 0-1)
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
-  // TSW_PLAN_AP=1: partial agent arrays in LDS (k_plan AP) when all do not fit. Off: on the full wh10k
-  // plan its rules rounds were 20 % faster (fire 3.27 -> 2.60 s) but movement pass 1 took 5.3 s
-  // instead of 0.25 s late in the plan (18.3 vs 13.8 s end to end), not yet explained
-  bool plan_ap = false;
+  bool occ_split = true;          // TSW_OCC_SPLIT=0: the occupancy grid goes to LDS only together with MU
   uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
@@ -105,7 +102,7 @@ struct Tunables {
     t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 16, t.dag_prefetch);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
-    t.plan_ap = num("TSW_PLAN_AP", 0, 1, 0) != 0;
+    t.occ_split = num("TSW_OCC_SPLIT", 0, 1, 1) != 0;
     t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
@@ -997,13 +994,14 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
   // without the agent arrays, the rules relabel's pointer-doubling buffers come next
-  // else the arrays every round touches (k_plan AP), else the pointer-doubling buffers
-  bool ap = !ag && c->tun.plan_ap && plan_lds_bytes(n, P.ncell, m, false, false, false, false, true) <= budget;
-  bool fl = !ag && !ap && c->tun.flinks_lds && plan_lds_bytes(n, P.ncell, m, false, false, false, true) <= budget;
-  bool oc = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, ap) <= budget;
-  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl, ap) <= budget;
+  bool fl = !ag && c->tun.flinks_lds && plan_lds_bytes(n, P.ncell, m, false, false, false, true) <= budget;
+  // the occupancy grid with the movement rounds' MU words, else OCC alone (every rules round reads
+  // OCC: C3's 170x84 fits OCC but not MU beside the agent arrays)
+  bool mu = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, true) <= budget;
+  bool oc = mu || (c->tun.occ_split && plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, false) <= budget);
+  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl, mu) <= budget;
   P.f_lds = fl;
-  P.agents_part = ap;
+  P.mu_lds = mu;
   P.agents_lds = ag;
   P.occ_lds = oc;
   P.tasks_lds = tk;
@@ -1031,7 +1029,7 @@ int build_occ(tsw_ctx* c, uint32_t n) {
 int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   *c->h_ctl = init;
   HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
-  size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds, P.agents_part);
+  size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds, P.mu_lds);
   // coop mode: the planner block reserves its CU's whole LDS so no worker wave is placed beside it
   // (they would compete for its SIMDs and LDS bandwidth on the critical path)
   if (P.coop) lds = std::max<size_t>(lds, (size_t)std::max(c->max_lds - 2048, 0));

@@ -47,7 +47,7 @@ struct PlanArgs {
   uint32_t mode, agents_lds, occ_lds, tasks_lds;
   uint32_t has_dups, prefetch;  // prefetch: enqueue rules-round next hops up front (rules_prefetch)
   uint32_t f_lds;               // F1/F2 carved in LDS although the agent arrays are global
-  uint32_t agents_part;         // AG false: V, G, SUCC, NHC, ONC, CANDC in LDS (k_plan AP)
+  uint32_t mu_lds;              // occ_lds and the movement rounds' MU words in LDS too
   uint32_t wave_rules_max;      // rules rounds run in wave 0 alone when n <= this
   uint32_t wide_prefetch;       // 0: off; else also (succ cell, goal) of every agent, path walked this many hops ahead
   uint32_t dag_prefetch;        // walk-ahead also queues the shortest-path successors of the first unresolved cell
@@ -96,7 +96,7 @@ struct PlanArgs {
 
 // flinks: the pointer-doubling buffers F1/F2 alone in LDS (when the agent arrays are not)
 size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks, bool flinks = false,
-                      bool partial = false);
+                      bool mu = true);
 hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, uint32_t* dups,
                       hipStream_t s);
 hipError_t launch_plan(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s);

@@ -703,9 +703,9 @@ __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
     }                                                \
   } while (0)
 
-// AG: every agent array in LDS. AP (AG false, n too large for AG): the arrays every rules round and
-// movement pass touches — V, G, SUCC, NHC, ONC, CANDC — in LDS, the rest (GT, DEC, MK, F1/F2) global.
-template <bool AG, bool OC, bool AP>
+// AG: every agent array in LDS. OC: the occupancy grid OCC in LDS; MUL: the movement rounds' MU
+// words too (OC alone fits grids whose MU does not, e.g. C3's 170x84 beside the agent arrays).
+template <bool AG, bool OC, bool MUL>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
@@ -739,18 +739,6 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     S.DEC = carve(n);
     S.ONC = carve(n);
     S.CANDC = carve(n);
-  } else if constexpr (AP) {
-    S.V = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
-    S.G = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
-    S.SUCC = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
-    S.NHC = carve(n);
-    S.ONC = carve(n);
-    S.CANDC = carve(n);
-    S.GT = P.gt;
-    S.F1 = P.f1;
-    S.F2 = P.f2;
-    S.DEC = P.dec;
-    S.MK = P.mk;
   } else {
     S.V = P.v;
     S.G = P.g;
@@ -771,7 +759,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   }
   if constexpr (OC) {
     S.OCC = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
-    S.MU = reinterpret_cast<uint64_t*>(carve((size_t)P.ncell * 8));
+    if constexpr (MUL) S.MU = reinterpret_cast<uint64_t*>(carve((size_t)P.ncell * 8));
+    else S.MU = P.mu;
   } else {
     S.OCC = P.occ;
     S.MU = P.mu;
@@ -795,9 +784,6 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       S.V[k] = P.v[k];
       S.G[k] = g;
       S.DEC[k] = P.dec[k];
-    } else if constexpr (AP) {
-      S.V[k] = P.v[k];
-      S.G[k] = g;
     }
     S.GT[k] = P.goal_tab[g];
     S.NHC[k] = NHC_DIRTY;
@@ -1820,11 +1806,6 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       P.g[k] = S.G[k];
       P.dec[k] = S.DEC[k];
     }
-  if constexpr (AP)
-    for (uint32_t k = tid; k < n; k += bd) {
-      P.v[k] = S.V[k];
-      P.g[k] = S.G[k];
-    }
   if constexpr (OC)
     for (uint32_t c = tid; c < P.ncell; c += bd) P.occ[c] = S.OCC[c];
   if (tid == 0) {
@@ -1866,13 +1847,12 @@ __global__ void k_occ_flag(uint32_t* occ, const uint32_t* cnt, uint32_t ncell, u
 }
 
 size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks, bool flinks,
-                      bool partial) {
+                      bool mu) {
   auto r16 = [](size_t b) { return (b + 15u) & ~(size_t)15u; };
   size_t b = r16(1024 * 4);
   if (agents) b += 4 * r16((size_t)n * 4) + 3 * r16((size_t)(n + 1) * 4) + 4 * r16(n);
-  else if (partial) b += 3 * r16((size_t)n * 4) + 3 * r16(n);
   else if (flinks) b += 2 * r16((size_t)(n + 1) * 4);
-  if (occ) b += r16((size_t)ncell * 4) + r16((size_t)ncell * 8);
+  if (occ) b += r16((size_t)ncell * 4) + (mu ? r16((size_t)ncell * 8) : 0u);
   if (tasks) b += r16((size_t)m * 4) + r16(m);
   return b;
 }
@@ -1885,20 +1865,21 @@ hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cn
   return hipGetLastError();
 }
 
-template <bool AG, bool OC, bool AP>
+template <bool AG, bool OC, bool MUL>
 static hipError_t launch_plan_t(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s) {
-  hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC, AP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC, MUL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_plan<AG, OC, AP>), dim3(1), dim3(block), lds, s, P);
+  hipLaunchKernelGGL((k_plan<AG, OC, MUL>), dim3(1), dim3(block), lds, s, P);
   return hipGetLastError();
 }
 
 hipError_t launch_plan(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s) {
+  const bool mu = P.occ_lds && P.mu_lds;
+  if (P.agents_lds && mu) return launch_plan_t<true, true, true>(P, lds, block, s);
   if (P.agents_lds && P.occ_lds) return launch_plan_t<true, true, false>(P, lds, block, s);
   if (P.agents_lds) return launch_plan_t<true, false, false>(P, lds, block, s);
-  if (P.agents_part && P.occ_lds) return launch_plan_t<false, true, true>(P, lds, block, s);
-  if (P.agents_part) return launch_plan_t<false, false, true>(P, lds, block, s);
+  if (mu) return launch_plan_t<false, true, true>(P, lds, block, s);
   if (P.occ_lds) return launch_plan_t<false, true, false>(P, lds, block, s);
   return launch_plan_t<false, false, false>(P, lds, block, s);
 }

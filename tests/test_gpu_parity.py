@@ -199,20 +199,32 @@ def test_mapd_block_paths(n, max_t):
     assert np.array_equal(rec, ref)
 
 
-@pytest.mark.parametrize("ap", ["1", "0"])
-def test_mapd_global_agent_arrays(ap, monkeypatch):
-    """6,000 agents: the agent arrays no longer fit LDS — the all-global variant (default,
-    pointer-doubling buffers carved in LDS on their own) and k_plan AP (TSW_PLAN_AP=1: the arrays
-    every round touches in LDS, the rest global) — lazy next hops with the wide prefetch on the
+def test_mapd_global_agent_arrays():
+    """6,000 agents: the agent arrays no longer fit LDS (global-memory k_plan variant, pointer-
+    doubling buffers carved in LDS on their own) — lazy next hops with the wide prefetch on the
     510x220 warehouse, a few timesteps, bit-exact."""
-    monkeypatch.setenv("TSW_PLAN_AP", ap)
     rows = maps.warehouse_map(510, 220, 0x510220)
     starts, tasks = maps.make_instance(rows, 6000, 18000, 0x6000)
     og = OracleGraph(maps.rows_to_array(rows))
-    ref, rgoal = og.mapd(starts, tasks, 4 if ap == "1" else 6, trace_goals=True)
+    ref, rgoal = og.mapd(starts, tasks, 4, trace_goals=True)
     with Planner(rows) as p:
-        rec, goal = p.plan_mapd_arrays(starts, tasks, 4 if ap == "1" else 6, trace_goals=True)
+        rec, goal = p.plan_mapd_arrays(starts, tasks, 4, trace_goals=True)
     assert rec.shape == ref.shape
+    assert np.array_equal(goal, rgoal)
+    assert np.array_equal(rec, ref)
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_mapd_occ_placement(split, monkeypatch):
+    """170x84 warehouse: the occupancy grid in LDS without the movement rounds' MU words (default,
+    k_plan<.., OC, !MUL>) and both in global memory (TSW_OCC_SPLIT=0), 400 agents, bit-exact."""
+    monkeypatch.setenv("TSW_OCC_SPLIT", split)
+    rows = maps.warehouse_map(170, 84, 0x170084)
+    starts, tasks = maps.make_instance(rows, 400, 1200, 0x400)
+    og = OracleGraph(maps.rows_to_array(rows))
+    ref, rgoal = og.mapd(starts, tasks, 150, trace_goals=True)
+    with Planner(rows) as p:
+        rec, goal = p.plan_mapd_arrays(starts, tasks, 150, trace_goals=True)
     assert np.array_equal(goal, rgoal)
     assert np.array_equal(rec, ref)
 
