@@ -111,10 +111,21 @@ __host__ __device__ __forceinline__ uint32_t blk_shared_u64(uint32_t nbp) {
 
 // WLS: the west-step blocks WL live in the wave's LDS (after V) instead of global scratch — no
 // memory-side atomics, at the cost of ~nbp*8 more LDS bytes per goal in flight.
-template <bool WLS>
+// PAIR: each 32-lane half of a wave runs its own goal (two goals per wave, in lockstep: both
+// halves start together, run levels until both BFS are done, then decode together). A level's
+// instruction stream then advances two goals; the level loop is bound by its dependent latency
+// chain (~3,250 cycles per level at 3 waves per SIMD for ~270 instructions), so halving the
+// instructions per goal-level costs little latency. LDS per goal is unchanged (goal slots, not
+// waves, are what LDS bounds); the global scratch (WL, anchors, list overflow) is per goal slot.
+template <bool WLS, bool PAIR>
 __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   extern __shared__ __align__(16) uint64_t smem64[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6, nwv = blockDim.x >> 6;
+  // goal slot of this lane: the half (PAIR) or the whole wave; NL lanes per goal, gl = lane in it
+  constexpr uint32_t NL = PAIR ? 32u : 64u;
+  const uint32_t hf = PAIR ? (lane >> 5) : 0u, gl = PAIR ? (lane & 31u) : lane;
+  const uint64_t hmask = PAIR ? (hf ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull) : ~0ull;
+  const uint32_t gs = PAIR ? 2u * wv + hf : wv;  // goal slot in the workgroup
   const uint32_t W = A.W, Bp = A.Bp, nbp = A.nbp, cap = A.cap, BW = A.BW;
   const uint32_t nfk = 1u << A.klog, kmask = nfk - 1u, klog = A.klog;
   uint64_t* FRs = smem64;
@@ -123,8 +134,12 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   uint64_t* WLl = nullptr;  // WLS: the LDS west-step blocks
   uint32_t* FL;  // 2 * nfk interleaved flag dwords: block t -> dword t & kmask, bit t >> klog
   uint16_t* LS;  // 2 * cap list entries / decode run table
+  uint16_t* CT;  // decode run table (PAIR: the wave's first goal slot's LS; ct_slot separates the halves)
   {
-    uint32_t* b = reinterpret_cast<uint32_t*>(smem64 + blk_shared_u64(nbp)) + wv * blk_bfs_words(nbp, nfk, cap, WLS);
+    uint32_t* b0 = reinterpret_cast<uint32_t*>(smem64 + blk_shared_u64(nbp));
+    uint32_t* b = b0 + gs * blk_bfs_words(nbp, nfk, cap, WLS);
+    uint32_t* bw = b0 + (PAIR ? 2u * wv : wv) * blk_bfs_words(nbp, nfk, cap, WLS);
+    CT = reinterpret_cast<uint16_t*>(bw + (WLS ? 4u : 2u) * ((nbp + 1u) & ~1u) + 2u * nfk);
     V = reinterpret_cast<uint64_t*>(b);
     if constexpr (WLS) {
       WLl = V + ((nbp + 1u) & ~1u);
@@ -139,7 +154,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   }
   __syncthreads();  // the only workgroup barrier: waves run their goals independently
 
-  const uint32_t gw = blockIdx.x * nwv + wv;
+  const uint32_t gw = PAIR ? 2u * (blockIdx.x * nwv + wv) + hf : blockIdx.x * nwv + wv;  // scratch slot
   uint16_t* anch = A.anch + (uint64_t)gw * A.nrs;  // compact anchors (run-start index)
   uint16_t* lovf = A.lovf + (uint64_t)gw * 2u * nbp;
   unsigned long long* WL = WLS ? reinterpret_cast<unsigned long long*>(WLl) : A.wlg + (uint64_t)gw * nbp;
@@ -148,20 +163,22 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
 
   for (;;) {
     uint32_t gi = 0;
-    if (lane == 0) gi = atomicAdd(A.work, 1u);
+    if (lane == 0) gi = atomicAdd(A.work, PAIR ? 2u : 1u);
     gi = __builtin_amdgcn_readfirstlane(gi);
     if (gi >= A.k) break;
+    gi += hf;                     // PAIR: the upper half takes the next goal
+    const bool live = gi < A.k;   // PAIR: the upper half of the last pair may have none
     const uint64_t t0 = clk();
-    const uint32_t goal = A.goals[gi];
-    const uint64_t slot = A.slots ? A.slots[gi] : gi;
+    const uint32_t goal = live ? A.goals[gi] : A.goals[gi - 1u];
+    const uint64_t slot = !live ? 0ull : A.slots ? A.slots[gi] : gi;
     const uint32_t gy = goal / W, gx = goal - gy * W;
     const uint32_t gpar = (gx + gy) & 1u;
 
-    for (uint32_t t = lane; t < nbp; t += 64u) {
+    for (uint32_t t = gl; t < nbp; t += NL) {
       V[t] = 0ull;
       WL[t] = 0ull;
     }
-    for (uint32_t t = lane; t < 2u * nfk; t += 64u) FL[t] = 0u;
+    for (uint32_t t = gl; t < 2u * nfk; t += NL) FL[t] = 0u;
     // the WL zeroing stores complete before this goal's atomics are issued
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -194,9 +211,9 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       w_e = w_e && !o_e;
       w_n = w_n && !o_n;
       w_s = w_s && !o_s;
-      const bool lds_only = nn + 5u * 64u <= cap;
+      const bool lds_only = nn + 5u * NL <= cap;
       auto append = [&](bool c, uint32_t entry) {
-        const uint64_t m = __ballot(c);
+        const uint64_t m = __ballot(c) & hmask;
         if (c) {
           const uint32_t pos = nn + lane_rank(m);
           if (lds_only) Ln[pos] = (uint16_t)entry;
@@ -278,9 +295,9 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       w0 = w0 && !o0;
       w1 = w1 && !o1;
       w2 = w2 && !o2;
-      const bool lds_only = nn + 3u * 64u <= cap;
+      const bool lds_only = nn + 3u * NL <= cap;
       auto append2 = [&](bool c, uint32_t entry) {
-        const uint64_t m = __ballot(c);
+        const uint64_t m = __ballot(c) & hmask;
         if (c) {
           const uint32_t pos = nn + lane_rank(m);
           if (lds_only) Ln[pos] = (uint16_t)entry;
@@ -298,7 +315,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
     {
       const uint32_t gp = ((gy >> 3) + 1u) * Bp + (gx >> 3);
       const uint64_t gm = 1ull << (((gy & 7u) << 3) | (gx & 7u));
-      const bool act = lane == 0u;
+      const bool act = gl == 0u && live;
       const uint32_t p = act ? gp : idle_p;
       const uint64_t nw = act ? gm : 0ull;
       const uint64_t f0 = FRs[p], fw = FRs[p - 1u], fe = FRs[p + 1u], fn = FRs[p - Bp], fs = FRs[p + Bp];
@@ -314,7 +331,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
     // ---- levels 1, 2, ...: process the blocks that gain cells at distance lvl -------------
     uint32_t cur = 0;
     uint32_t lvl = 1;
-    while (ncur != 0u) {
+    while (PAIR ? __ballot(ncur != 0u) != 0ull : ncur != 0u) {
       if (lvl >= 0xFFFFu) {
         if (lane == 0) atomicOr(A.err, ERR_DIST_OVERFLOW);
         break;
@@ -378,30 +395,34 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         push2(p, nw, vv, f0, fw, fe, fx, fp, vw, ve, vx, vp, Fn, Ln, On);
         ++n_chunk;
       };
-      if (ncur <= 32u && ncur <= cap) {
+      // path choice and trip counts are wave-uniform (PAIR: over both halves' lists)
+      const uint32_t nmax = PAIR ? max((uint32_t)__builtin_amdgcn_readlane((int)ncur, 0),
+                                       (uint32_t)__builtin_amdgcn_readlane((int)ncur, 32))
+                                 : ncur;
+      if (nmax <= NL / 2u && nmax <= cap) {
         // few active blocks: lane pairs, one half-block per lane (a single chunk)
-        const uint32_t j0 = lane >> 1;
+        const uint32_t j0 = gl >> 1;
         chunk2(j0 < ncur ? (uint32_t)Lc[j0] : idle_p, j0 < ncur);
-      } else if (ncur <= cap) {
+      } else if (nmax <= cap) {
         // LDS-only list (wave-uniform): no global load in the loop, so nothing waits for the
         // wave's outstanding anchor stores; entries prefetched one chunk ahead
-        uint32_t e_next = lane < ncur ? (uint32_t)Lc[lane] : idle_p;
-        for (uint32_t b0 = 0; b0 < ncur; b0 += 64u) {
+        uint32_t e_next = gl < ncur ? (uint32_t)Lc[gl] : idle_p;
+        for (uint32_t b0 = 0; b0 < nmax; b0 += NL) {
           const uint32_t p = e_next;
-          const uint32_t i = b0 + 64u + lane;
+          const uint32_t i = b0 + NL + gl;
           e_next = i < ncur ? (uint32_t)Lc[i] : idle_p;
-          chunk(p, b0 + lane < ncur);
+          chunk(p, b0 + gl < ncur);
         }
       } else {
-        for (uint32_t b0 = 0; b0 < ncur; b0 += 64u) {
-          const uint32_t i = b0 + lane;
+        for (uint32_t b0 = 0; b0 < nmax; b0 += NL) {
+          const uint32_t i = b0 + gl;
           const uint32_t p = i >= ncur ? idle_p : i < cap ? (uint32_t)Lc[i] : ld_nc16(Oc + (i - cap));
           chunk(p, i < ncur);
         }
       }
       // the flags of this level's list are reused two levels later
-      for (uint32_t t = lane; t < nfk; t += 64u) Fc[t] = 0u;
-      if (nn > cap) full_sync();  // overflow entries went to global memory
+      for (uint32_t t = gl; t < nfk; t += NL) Fc[t] = 0u;
+      if (PAIR ? __ballot(nn > cap) != 0ull : nn > cap) full_sync();  // overflow entries went to global memory
       else lds_sync();
       cur = nxt;
       ncur = nn;
@@ -476,19 +497,19 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
           const uint32_t sj = rs ? (uint32_t)__builtin_ctz(rs) : 0u;
           rs &= rs - 1u;
           const uint32_t Fs = 2u * __popc(wl & (0xFFFFFFFFu >> (31u - sj))) - (sj + 1u);
-          LS[ct_slot(lane, j)] = (uint16_t)(cu.a[j - 1u] - Fs);  // own column: program order suffices
+          CT[ct_slot(lane, j)] = (uint16_t)(cu.a[j - 1u] - Fs);  // own column: program order suffices
         }
         for (uint32_t j = 5; rs != 0u; ++j) {
           const uint32_t sj = __builtin_ctz(rs);
           rs &= rs - 1u;
           const uint32_t Aj = ld_nc16(anch + aidx(p0 + (sj >> 3), sj >> 3, r * 8u + (sj & 7u)));
           const uint32_t Fs = 2u * __popc(wl & (0xFFFFFFFFu >> (31u - sj))) - (sj + 1u);
-          LS[ct_slot(lane, j)] = (uint16_t)(Aj - Fs);
+          CT[ct_slot(lane, j)] = (uint16_t)(Aj - Fs);
         }
 #pragma unroll
         for (int b = 0; b < 32; ++b) {
           const uint32_t m = 0xFFFFFFFFu >> (31 - b);
-          const uint32_t C = LS[ct_slot(lane, (uint32_t)__popc(rsw & m))];
+          const uint32_t C = CT[ct_slot(lane, (uint32_t)__popc(rsw & m))];
           const uint32_t F = 2u * __popc(wl & m) - (uint32_t)(b + 1);
           const uint32_t v = ((vis >> b) & 1u) ? ((F + C) & 0xFFFFu) : 0xFFFFu;
           if (b & 1) pk[b >> 1] |= v << 16;
@@ -527,6 +548,45 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       const uint32_t x0 = cu.cw << 5;
       const uint32_t cnt = valid ? min(32u, W - x0) : 0u;
       const uint32_t cb = cu.y * W + x0;
+      if constexpr (PAIR) {
+        // each half stages its own goal's 32 words kb..kb+31 into its own LS and stores them with
+        // its own 32 lanes (512 B per store instruction per half)
+        if (kb >= nwords) return;  // wave-uniform
+        const uint32_t ll = min(31u, nwords - 1u - kb);
+        const uint32_t cs = hf ? (uint32_t)__builtin_amdgcn_readlane((int)cb, 32)
+                               : (uint32_t)__builtin_amdgcn_readlane((int)cb, 0);
+        const uint32_t ce = hf ? (uint32_t)__builtin_amdgcn_readlane((int)(cb + cnt), (int)(32u + ll))
+                               : (uint32_t)__builtin_amdgcn_readlane((int)(cb + cnt), (int)ll);
+        const uint32_t base = cs & ~7u;
+        if (valid) {
+          const uint32_t off = cb - base;
+          if ((W & 31u) == 0u) {
+            uint4* q = reinterpret_cast<uint4*>(LS + off);
+            q[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            q[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+            q[2] = make_uint4(pk[8], pk[9], pk[10], pk[11]);
+            q[3] = make_uint4(pk[12], pk[13], pk[14], pk[15]);
+          } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 32u; ++b)
+              if (b < cnt) LS[off + b] = (uint16_t)(pk[b >> 1] >> ((b & 1u) * 16u));
+          }
+        }
+        lds_sync();
+        const uint32_t nch = live ? (ce - base + 7u) >> 3 : 0u;
+        for (uint32_t q = gl; q < nch; q += 32u) {
+          const uint32_t c0 = base + 8u * q;
+          if (c0 >= cs && c0 + 8u <= ce) {
+            *reinterpret_cast<uint4*>(D + c0) = *reinterpret_cast<const uint4*>(LS + 8u * q);
+          } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 8u; ++b)
+              if (c0 + b >= cs && c0 + b < ce) D[c0 + b] = LS[8u * q + b];
+          }
+        }
+        lds_sync();
+        return;
+      }
 #pragma unroll
       for (uint32_t hh = 0; hh < 2u; ++hh) {
         const uint32_t fl = 32u * hh;
@@ -580,28 +640,30 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
     // four words in flight per lane (ring w0..w3, fetch distance 4): a decode waits on loads
     // issued three decodes earlier, enough to cover L2 latency at this residency. The loop is
     // wave-uniform (the staged write-out is a wave-wide exchange); lanes past the end idle.
+    // (PAIR: per half, NL = 32 lanes; a half without a goal decodes nothing and stores nothing)
     Word w0{}, w1{}, w2{}, w3{};
-    if (lane < nwords) fetch(lane, w0);
-    if (lane + 64u < nwords) fetch(lane + 64u, w1);
-    if (lane + 128u < nwords) fetch(lane + 128u, w2);
-    if (lane + 192u < nwords) fetch(lane + 192u, w3);
-    for (uint32_t kb = 0; kb < nwords; kb += 256u) {
-      const uint32_t k = kb + lane;
-      emit(w0, k < nwords, kb);
-      if (k + 256u < nwords) fetch(k + 256u, w0);
-      if (kb + 64u < nwords) emit(w1, k + 64u < nwords, kb + 64u);
-      if (k + 320u < nwords) fetch(k + 320u, w1);
-      if (kb + 128u < nwords) emit(w2, k + 128u < nwords, kb + 128u);
-      if (k + 384u < nwords) fetch(k + 384u, w2);
-      if (kb + 192u < nwords) emit(w3, k + 192u < nwords, kb + 192u);
-      if (k + 448u < nwords) fetch(k + 448u, w3);
+    const uint32_t nwl = live ? nwords : 0u;  // words of this lane's goal
+    if (gl < nwl) fetch(gl, w0);
+    if (gl + NL < nwl) fetch(gl + NL, w1);
+    if (gl + 2u * NL < nwl) fetch(gl + 2u * NL, w2);
+    if (gl + 3u * NL < nwl) fetch(gl + 3u * NL, w3);
+    for (uint32_t kb = 0; kb < nwords; kb += 4u * NL) {
+      const uint32_t k = kb + gl;
+      emit(w0, k < nwl, kb);
+      if (k + 4u * NL < nwl) fetch(k + 4u * NL, w0);
+      if (kb + NL < nwords) emit(w1, k + NL < nwl, kb + NL);
+      if (k + 5u * NL < nwl) fetch(k + 5u * NL, w1);
+      if (kb + 2u * NL < nwords) emit(w2, k + 2u * NL < nwl, kb + 2u * NL);
+      if (k + 6u * NL < nwl) fetch(k + 6u * NL, w2);
+      if (kb + 3u * NL < nwords) emit(w3, k + 3u * NL < nwl, kb + 3u * NL);
+      if (k + 7u * NL < nwl) fetch(k + 7u * NL, w3);
     }
     lds_sync();  // the next goal re-initialises this wave's LDS
     if (A.prof) {
       const uint64_t t2 = clk();
       t_bfs += t1 - t0;
       t_dec += t2 - t1;
-      n_lvl += lvl;
+      n_lvl += PAIR ? (uint64_t)lvl * (uint64_t)__popcll(__ballot(live && gl == 0u)) : lvl;
     }
   }
   if (A.prof && lane == 0) {
@@ -618,8 +680,8 @@ uint32_t bfs_blk_klog(uint32_t nbp) {
   return kl;
 }
 
-uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds, bool wls) {
-  const size_t per_wave = (size_t)blk_bfs_words(nbp, 1u << bfs_blk_klog(nbp), cap, wls) * 4u;
+uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds, bool wls, bool pair) {
+  const size_t per_wave = (size_t)blk_bfs_words(nbp, 1u << bfs_blk_klog(nbp), cap, wls) * 4u * (pair ? 2u : 1u);
   const size_t shared = (size_t)blk_shared_u64(nbp) * 8u;  // FR u64 + AB u32
   if (max_lds <= 0 || shared + per_wave > (size_t)max_lds) return 0;
   return (uint32_t)std::min<size_t>(16u, ((size_t)max_lds - shared) / per_wave);
@@ -630,19 +692,24 @@ hipError_t launch_bfs_blk(const BlkBfsArgs& A0, int max_lds, int num_cu, hipStre
   BlkBfsArgs A = A0;
   A.klog = bfs_blk_klog(A.nbp);
   A.bp_magic = (uint32_t)((0xFFFFFFFFull + A.Bp) / A.Bp);  // ceil(2^32 / Bp): exact p / Bp for p*Bp < 2^32
-  const bool wls = A.wls != 0u;
-  const size_t per_wave = (size_t)blk_bfs_words(A.nbp, 1u << A.klog, A.cap, wls) * 4u;
+  const bool wls = A.wls != 0u, pair = A.pair != 0u;
+  const uint32_t gpw = pair ? 2u : 1u;  // goal slots per wave
+  const size_t per_wave = (size_t)blk_bfs_words(A.nbp, 1u << A.klog, A.cap, wls) * 4u * gpw;
   const size_t shared = (size_t)blk_shared_u64(A.nbp) * 8u;  // FR u64 + AB u32
-  const uint32_t nwv = std::min<uint32_t>(A.max_waves, bfs_blk_waves_per_block(A.nbp, A.cap, max_lds, wls));
+  const uint32_t nwv = std::min<uint32_t>(A.max_waves, bfs_blk_waves_per_block(A.nbp, A.cap, max_lds, wls, pair));
   if (nwv == 0 || A.nbp > 0x10000u || A.cap > 0x8000u) return hipErrorInvalidValue;
-  const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cu, (A.k + nwv - 1u) / nwv));
-  if ((uint64_t)grid * nwv > A.scratch_waves) return hipErrorInvalidValue;
+  const uint32_t grid =
+      std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cu, (A.k + gpw * nwv - 1u) / (gpw * nwv)));
+  if ((uint64_t)grid * nwv * gpw > A.scratch_waves) return hipErrorInvalidValue;  // scratch per goal slot
   const size_t lds = shared + nwv * per_wave;
-  const void* fn = wls ? (const void*)k_bfs_blk<true> : (const void*)k_bfs_blk<false>;
+  const void* fn = wls ? (pair ? (const void*)k_bfs_blk<true, true> : (const void*)k_bfs_blk<true, false>)
+                       : (pair ? (const void*)k_bfs_blk<false, true> : (const void*)k_bfs_blk<false, false>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  if (wls) hipLaunchKernelGGL(k_bfs_blk<true>, dim3(grid), dim3(nwv * 64u), lds, s, A);
-  else hipLaunchKernelGGL(k_bfs_blk<false>, dim3(grid), dim3(nwv * 64u), lds, s, A);
+  if (wls && pair) hipLaunchKernelGGL((k_bfs_blk<true, true>), dim3(grid), dim3(nwv * 64u), lds, s, A);
+  else if (wls) hipLaunchKernelGGL((k_bfs_blk<true, false>), dim3(grid), dim3(nwv * 64u), lds, s, A);
+  else if (pair) hipLaunchKernelGGL((k_bfs_blk<false, true>), dim3(grid), dim3(nwv * 64u), lds, s, A);
+  else hipLaunchKernelGGL((k_bfs_blk<false, false>), dim3(grid), dim3(nwv * 64u), lds, s, A);
   return hipGetLastError();
 }
 

@@ -57,6 +57,7 @@ struct Tunables {
   bool bfs_nostage = false;       // TSW_BFS_NOSTAGE: k_bfs_blk writes rows lane-strided (no LDS staging)
   uint32_t bfs_dbg = 0;           // TSW_BFS_DBG: k_bfs_blk diagnostics (BlkBfsArgs::dbg)
   uint32_t bfs_wls = 0;           // TSW_BFS_WLS: k_bfs_blk west-step blocks in LDS
+  uint32_t bfs_pair = 0;          // TSW_BFS_PAIR: k_bfs_blk two goals per wave (one per 32-lane half)
   uint32_t wave_hcap = 0;         // TSW_ASTAR_WAVE_HCAP: k_astar_wave LDS heap entries (0 = default)
   int astar_global_gs = -1;       // TSW_ASTAR_GLOBAL_GS: -1 auto, 0 LDS g-scores, 1 global slots
   bool astar_tier2 = true;        // TSW_ASTAR_NO_TIER2: skip the LDS-heap/global-g second tier
@@ -92,6 +93,7 @@ struct Tunables {
     t.bfs_nostage = getenv("TSW_BFS_NOSTAGE") != nullptr;
     t.bfs_dbg = (uint32_t)num("TSW_BFS_DBG", 0, 7, 0);
     t.bfs_wls = (uint32_t)num("TSW_BFS_WLS", 0, 1, t.bfs_wls);
+    t.bfs_pair = (uint32_t)num("TSW_BFS_PAIR", 0, 1, t.bfs_pair);
     t.wave_hcap = (uint32_t)num("TSW_ASTAR_WAVE_HCAP", 4, 1 << 20, 0);
     t.astar_global_gs = (int)num("TSW_ASTAR_GLOBAL_GS", 0, 1, -1);
     t.astar_tier2 = getenv("TSW_ASTAR_NO_TIER2") == nullptr;
@@ -612,12 +614,21 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   const uint32_t max_waves = c->tun.bfs_waves;
   const uint32_t bfs_mode = c->tun.bfs_mode;
   uint32_t nbw = 0;
-  if ((bfs_mode == 0 || bfs_mode == 3) && c->nbp <= 0x10000u)
-    nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->tun.blk_cap, c->max_lds, c->tun.bfs_wls != 0u));
+  // two goals per wave only where two goal slots per wave fit LDS, else one
+  bool pair = c->tun.bfs_pair != 0u;
+  if ((bfs_mode == 0 || bfs_mode == 3) && c->nbp <= 0x10000u) {
+    nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->tun.blk_cap, c->max_lds, c->tun.bfs_wls != 0u, pair));
+    if (nbw == 0 && pair) {
+      pair = false;
+      nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->tun.blk_cap, c->max_lds, c->tun.bfs_wls != 0u, false));
+    }
+  }
   if (nbw == 0 && bfs_mode == 3) RET(TSW_EINVAL, "k_bfs_blk does not fit this grid (TSW_BFS_KERNEL=blk)");
   if (nbw > 0) {
     Timer t(c, CAT_BFS);
-    TRY(ensure_wave_scratch(c, (uint64_t)c->num_cu * nbw, std::max<size_t>(c->nrs, 1), (size_t)c->nbp * 2u));
+    // scratch per goal slot: one per wave, two with TSW_BFS_PAIR
+    TRY(ensure_wave_scratch(c, (uint64_t)c->num_cu * nbw * (pair ? 2u : 1u), std::max<size_t>(c->nrs, 1),
+                            (size_t)c->nbp * 2u));
     if (c->wlg_waves < c->wave_scratch) {
       HIPCHK(hipStreamSynchronize(c->s));
       if (c->d_wlg) HIPCHK(hipFree(c->d_wlg));
@@ -651,6 +662,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     A.stage = (dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u && !c->tun.bfs_nostage) ? 1u : 0u;
     A.dbg = c->tun.bfs_dbg;
     A.wls = c->tun.bfs_wls;
+    A.pair = pair ? 1u : 0u;
     A.max_waves = nbw;
     A.scratch_waves = std::min(c->wave_scratch, c->wlg_waves);
     A.prof = (uint64_t*)bfs_prof_buf(c);

@@ -59,12 +59,14 @@ struct BlkBfsArgs {
   uint32_t stage;         // tables 16-B aligned (dist, dstride % 8 == 0): decoded rows leave through an
                           // LDS staging pass as coalesced 16-B stores (any W)
   uint32_t max_waves;
-  uint64_t scratch_waves;
+  uint64_t scratch_waves;  // goal slots (waves, or 2 per wave with pair) the scratch is sized for
   uint64_t* prof;         // optional: [bfs cycles, decode cycles, levels, chunks] summed over waves
   uint32_t dbg;           // TSW_BFS_DBG (diagnostics): 1 nontemporal table stores, 2 no WL atomics, 4 no anchors
-  uint32_t wls;           // west-step blocks in LDS (k_bfs_blk<true>) instead of global scratch
+  uint32_t wls;           // west-step blocks in LDS (k_bfs_blk<true, *>) instead of global scratch
+  uint32_t pair;          // two goals per wave, one per 32-lane half (k_bfs_blk<*, true>)
 };
-uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds, bool wls);
+// waves per workgroup that fit LDS (pair: two goal slots per wave)
+uint32_t bfs_blk_waves_per_block(uint32_t nbp, uint32_t cap, int max_lds, bool wls, bool pair);
 hipError_t launch_bfs_blk(const BlkBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
 
 // K1 v4 (tsw_bfs_big.hip): one WORKGROUP per goal over 8x8 cell blocks, free blocks and run

@@ -80,6 +80,23 @@ def test_bfs_blk_lds_west_steps(name):
     _check(rows, _goals(rows, 40, 9), TSW_BFS_KERNEL="blk", TSW_BFS_WLS=1)
 
 
+@pytest.mark.parametrize("wls", [0, 1])
+@pytest.mark.parametrize("name", sorted(GRIDS))
+def test_bfs_blk_pair(name, wls):
+    """k_bfs_blk with two goals per wave, one per 32-lane half (TSW_BFS_PAIR=1). An odd goal count
+    leaves the upper half of the last pair without a goal (it must write nothing)."""
+    rows = GRIDS[name]()
+    _check(rows, _goals(rows, 41, 13), TSW_BFS_KERNEL="blk", TSW_BFS_PAIR=1, TSW_BFS_WLS=wls)
+
+
+@pytest.mark.parametrize("cap", [1, 3, 17])
+def test_bfs_blk_pair_list_overflow(cap):
+    """Two goals per wave with lists spilling to the per-goal-slot global overflow area; halves
+    whose lists differ in length run different trip counts inside one level."""
+    rows = maps.cave_map(128, 97, 9)
+    _check(rows, _goals(rows, 25, 3), TSW_BFS_KERNEL="blk", TSW_BFS_BLKCAP=cap, TSW_BFS_PAIR=1)
+
+
 @pytest.mark.parametrize("cap", [1, 3, 17])
 def test_bfs_wave_list_overflow(cap):
     """Lists longer than the LDS capacity spill to the per-wave global overflow area."""
@@ -94,7 +111,7 @@ def test_bfs_blk_list_overflow(cap, wls):
     _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="blk", TSW_BFS_BLKCAP=cap, TSW_BFS_WLS=wls)
 
 
-@pytest.mark.parametrize("kernel", ["blk", "wave", "big"])
+@pytest.mark.parametrize("kernel", ["blk", "blk-pair", "wave", "big"])
 def test_bfs_wave_unreachable_pockets(kernel):
     """Walled-off pockets stay 0xFFFF; goals inside a pocket see only the pocket."""
     a = np.zeros((40, 70), dtype=bool)
@@ -105,7 +122,10 @@ def test_bfs_wave_unreachable_pockets(kernel):
     cells = maps.rows_to_array(rows)
     goals = np.array([0, 69, 11 * 70 + 5, 22 * 70 + 32, 39 * 70 + 69], dtype=np.uint32)
     assert all(cells.reshape(-1)[g] != ord("@") for g in goals)
-    _check(rows, goals, TSW_BFS_KERNEL=kernel)
+    if kernel == "blk-pair":
+        _check(rows, goals, TSW_BFS_KERNEL="blk", TSW_BFS_PAIR=1)
+    else:
+        _check(rows, goals, TSW_BFS_KERNEL=kernel)
 
 
 class _DevBuf:
@@ -131,7 +151,7 @@ class _DevBuf:
         self.hip.hipFree(self.ptr)
 
 
-@pytest.mark.parametrize("kernel", ["blk", "wave", "big"])
+@pytest.mark.parametrize("kernel", ["blk", "blk-pair", "wave", "big"])
 def test_bfs_den520d_full_size(kernel):
     """BASELINE configs[3] geometry: 256x257 cave, 1,000 distinct goals through the device-output
     entry point the bench times (16-B stores), every table bit-exact vs the oracle."""
@@ -140,7 +160,8 @@ def test_bfs_den520d_full_size(kernel):
     og = OracleGraph(cells)
     goals = np.sort(_goals(rows, 1000, 0x520D))
     ncell = 256 * 257
-    with _env(TSW_BFS_KERNEL=kernel), Planner(rows) as p:
+    env = dict(TSW_BFS_KERNEL="blk", TSW_BFS_PAIR=1) if kernel == "blk-pair" else dict(TSW_BFS_KERNEL=kernel)
+    with _env(**env), Planner(rows) as p:
         buf = _DevBuf(goals.size * ncell * 2)
         p.dist_tables_device(goals, buf.ptr.value)
         got = buf.to_host(np.empty((goals.size, ncell), dtype=np.uint16))
