@@ -15,6 +15,8 @@
 #   astar        scripts/astar_bench.py                                -> gpurun_out/astar_bench.json
 #   bfs          scripts/bfs_bench.py (K1 cells/s, den520d + 1024^2) -> gpurun_out/bfs_bench.log
 #   rehearse2    bench.py at N=2 on one GPU over gloo                  -> gpurun_out/rehearse2.json
+#   bfsocc       scripts/bfs_occ_probe.sh (K1 residency / PAIR probe)  -> gpurun_out/bfs_occ.log
+#   abplan       scripts/ab_plan.sh with the defaults (planner section clocks) -> gpurun_out/ab_0.json/.err
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -27,8 +29,9 @@ for step in "$@"; do
   case $step in
     tests|tests:*)
       k=""; [ "$step" != tests ] && k="-k ${step#tests:}"
-      run 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread $k > gpurun_out/gpu_tests.log 2>&1
-      rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -le 1 ] || exit $rc ;;
+      log=gpurun_out/gpu_tests.log; [ "$step" != tests ] && log=gpurun_out/gpu_tests_k.log
+      run 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread $k > $log 2>&1
+      rc=$?; tail -3 $log; [ $rc -le 1 ] || exit $rc ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $? ;;
     bench) run 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $? ;;
     plan) run 300 python bench.py --steps 3 --warmup 1 --no-cpu --no-bfs > gpurun_out/plan.json 2> gpurun_out/plan.err || exit $? ;;
@@ -42,6 +45,8 @@ for step in "$@"; do
     rehearse2) run 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu --dist-backend gloo \
         > gpurun_out/rehearse2.json 2> gpurun_out/rehearse2.log || exit $? ;;
+    bfsocc) bash scripts/bfs_occ_probe.sh || exit $? ;;
+    abplan) bash scripts/ab_plan.sh "TSW_X=0" || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
