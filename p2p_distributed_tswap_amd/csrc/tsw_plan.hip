@@ -140,7 +140,12 @@ __device__ __forceinline__ uint32_t succ_of(const PlanArgs& P, const Arrays& S, 
 // a cycle (length >= 2) of succ over not-at-goal agents. Pointer doubling: after R rounds
 // with 2^R > n, F(k) = succ^(2^R)(k) sits on the cycle k drains into (or the sink n), and
 // succ^(2^R) permutes each cycle, so {F(k)} is exactly the set of cycle members.
-__device__ void rules_init(const PlanArgs& P, const Arrays& S) {
+// pf (phase start, wide prefetch): rules_prefetch fused into the first pass — the pair (cell of
+// succ(k), goal of k) is the CANDC load itself, and k's own next pair is one more load — saving the
+// separate block-wide pass and its repeated table reads.
+__device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q);
+__device__ __forceinline__ bool spec_full(const PlanArgs& P, const uint32_t* s_q);
+__device__ void rules_init(const PlanArgs& P, const Arrays& S, uint32_t* pf = nullptr) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x, n = P.n;
   for (uint32_t k = tid; k < n; k += bd) {
     const uint32_t s = succ_of(P, S, k);
@@ -148,9 +153,19 @@ __device__ void rules_init(const PlanArgs& P, const Arrays& S) {
     S.F1[k] = s == SUCC_TERM ? n : s;
     S.ONC[k] = 0;
     uint8_t cc = NHC_DIRTY;
-    if (s != SUCC_TERM && s != k && S.GT[k] >= 0)
-      cc = P.nh[(uint64_t)S.GT[k] * P.nstride + S.V[s]];
+    const int32_t tab = S.GT[k];
+    if (s != SUCC_TERM && s != k && tab >= 0)
+      cc = P.nh[(uint64_t)tab * P.nstride + S.V[s]];
     S.CANDC[k] = cc;
+    if (pf && tab >= 0 && !spec_full(P, pf)) {  // as rules_prefetch (wide mode: no ONC filter)
+      const uint8_t c = S.NHC[k];
+      const uint32_t g = S.G[k];
+      if (c < NH_STAY && S.V[k] != g) {
+        const uint32_t u = step_cell(S.V[k], c, P.W);
+        if (u != g && P.nh[(uint64_t)tab * P.nstride + u] == NH_UNKNOWN) prefetch_pair(P, u, g, tab, pf);
+      }
+      if (cc == NH_UNKNOWN) prefetch_pair(P, S.V[s], g, tab, pf);
+    }
   }
   if (tid == 0) {
     S.F1[n] = n;
@@ -355,9 +370,15 @@ __device__ __forceinline__ bool plan_abort(const PlanArgs& P) {
   return P.hflags && __hip_atomic_load(&P.hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
 }
 
-// thread 0: make every entry queued so far visible to the workers (caller: after a barrier)
+// thread 0: make every entry queued so far visible to the workers (caller: after a barrier). A publish
+// whose heads equal the last published ones is skipped: no entry and no PENDING mark was written since
+// (marks are only written with an entry), and the agent-scope release it would cost writes back this
+// XCD's L2. s_q[3] / s_q[4] hold the last published heads (0 = the launch's zeroed CoopCtl).
 __device__ __forceinline__ void coop_publish(const PlanArgs& P, uint32_t* s_q) {
   const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap);
+  if (hn == s_q[3] && hs == s_q[4]) return;
+  s_q[3] = hn;
+  s_q[4] = hs;
   __hip_atomic_store(&P.cc->head_s, hs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&P.cc->head_n, hn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   // wake idle workers, which poll only this word (a plain agent-scope store of a new value)
@@ -709,7 +730,7 @@ template <bool AG, bool OC, bool MUL>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[3], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
+  __shared__ uint32_t s_q[5], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[32], s_tlast, s_tp;
@@ -800,6 +821,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     s_q[1] = 0;  // speculative queue (coop mode)
     s_q[2] = 0;  // publishes (coop mode)
+    s_q[3] = 0;  // last published needed / speculative heads (coop mode)
+    s_q[4] = 0;
     for (int k = 0; k < 32; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
@@ -882,6 +905,19 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                   S.G[ai] = ng;
                   S.GT[ai] = P.goal_tab[ng];
                   S.NHC[ai] = NHC_DIRTY;
+                  // coop: the workers predict the task this agent takes when it becomes idle at ng
+                  // (published with this step's PRE1 queue)
+                  if (P.coop && P.predict_k) {
+                    const uint32_t qi = atomicAdd(&s_q[1], 1u);
+                    if (qi < P.qscap) {
+                      AstarQuery q;
+                      q.v = ng;
+                      q.goal = PREDICT_JOB;
+                      q.tab = -1;
+                      q.out = qi;
+                      P.QS[qi] = q;
+                    }
+                  }
                 }
               } else if (st == ST_TO_DELIVERY) {
                 st = ST_IDLE;
@@ -975,14 +1011,15 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
       // one through s. CANDC[k] prefetches s's next hop toward k's goal for every rule-3
       // candidate k, so a swap needs no global round trip on the serial path.
       if (P.dbg && tid == 0) s_tp = wall_clock64();
-      rules_init(P, S);
+      const bool fuse_pf = P.prefetch && P.wide_prefetch;  // rules_prefetch inside the first pass
+      rules_init(P, S, fuse_pf ? s_q : nullptr);
       if (tid == 0) s_ctl.relabel_full += 1;
       if (P.dbg && tid == 0) {
         const unsigned long long nw = wall_clock64();
         s_tick[26] += nw - s_tp;
         s_tp = nw;
       }
-      if (P.prefetch) rules_prefetch(P, S, s_q);
+      if (P.prefetch && !fuse_pf) rules_prefetch(P, S, s_q);
       if (P.dbg && tid == 0) {
         const unsigned long long nw = wall_clock64();
         s_tick[27] += nw - s_tp;
