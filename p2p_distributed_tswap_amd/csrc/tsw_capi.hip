@@ -74,7 +74,6 @@ struct Tunables {
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
   bool task_chains = true;        // TSW_TASK_CHAINS=0: no task-chain jobs for the coop workers
   bool chain_preempt = true;      // TSW_CHAIN_PREEMPT=0: chain workers finish a chain before serving queued pairs
-  uint32_t predict_k = 4;         // TSW_PREDICT_K: coop workers resolve (delivery, pickup) for the K nearest unused tasks at each pickup (0: off)
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
 
   static Tunables from_env() {
@@ -111,7 +110,6 @@ struct Tunables {
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
     t.task_chains = num("TSW_TASK_CHAINS", 0, 1, 1) != 0;
     t.chain_preempt = num("TSW_CHAIN_PREEMPT", 0, 1, 1) != 0;
-    t.predict_k = (uint32_t)num("TSW_PREDICT_K", 0, 8, t.predict_k);
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
     return t;
   }
@@ -1025,7 +1023,6 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   if (P.coop) {
     P.QS = c->d_QS;
     P.qscap = (uint32_t)c->qscap;
-  P.predict_k = P.mode == MODE_MAPD && P.m > 0 ? c->tun.predict_k : 0u;
     P.cc = c->d_cc;
   }
   return P;
@@ -1067,12 +1064,6 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     // are larger), the rest stay free for the pairs the planner waits on
     W.tmask = P.n > 2000u ? 3u : 1u;
     W.preempt = c->tun.chain_preempt ? 1u : 0u;
-    W.pick_xy = c->d_pick_xy;
-    W.used = c->d_used;
-    W.pick = c->d_pick;
-    W.goal_tab = c->d_goal_tab;
-    W.m = P.mode == MODE_MAPD ? P.m : 0u;
-    W.predict_k = W.m ? c->tun.predict_k : 0u;
     W.hflags = c->d_flags;
     W.gs_all = c->d_gs;
     W.epochs = c->d_epochs;
@@ -1198,10 +1189,9 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                   (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
           fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u\n",
                   cc.waits ? (double)cc.dbg_depth / cc.waits : 0.0, cc.dbg_depth_max);
-          fprintf(stderr, "[k_plan] worker A* ms (queries): needed %.1f (%u) spec %.1f (%u) task chains %.1f (%u) "
-                  "assignment predictions %.1f (%u)\n",
+          fprintf(stderr, "[k_plan] worker A* ms (queries): needed %.1f (%u) spec %.1f (%u) task chains %.1f (%u)\n",
                   cc.wbusy[0] / (double)c->wall_khz, cc.wcount[0], cc.wbusy[1] / (double)c->wall_khz, cc.wcount[1],
-                  cc.wbusy[2] / (double)c->wall_khz, cc.wcount[2], cc.wbusy[3] / (double)c->wall_khz, cc.wcount[3]);
+                  cc.wbusy[2] / (double)c->wall_khz, cc.wcount[2]);
         }
       }
       // exit mode: pairs the prefetch queued but no firing needed — resolve them so no table entry

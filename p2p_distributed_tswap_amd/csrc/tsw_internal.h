@@ -80,10 +80,6 @@ struct CoopCtl {
   uint32_t dbg_depth_max, pad4[3];
 };
 
-// speculative-queue entry that is not a pair but an assignment prediction job (coop mode): v = the
-// delivery cell an agent will become idle at, goal = PREDICT_JOB
-constexpr uint32_t PREDICT_JOB = 0xFFFFFFFFu;
-
 struct AstarQuery {
   uint32_t v;     // start cell
   uint32_t goal;  // goal cell

@@ -1405,67 +1405,6 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
     const uint32_t w = w_ld(reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u));
     return (uint8_t)(w >> (8u * (uint32_t)((uintptr_t)p & 3u)));
   };
-  // Assignment prediction (tswap.rs:125-137): an agent that reaches its delivery cell d becomes idle
-  // there and takes the unused task whose pickup is nearest by Manhattan distance (first minimum by
-  // index). The planner queues a job for d when the agent picks its task up — tens of steps before the
-  // assignment — and the worker resolves get_path(d, p)[1] for the K nearest unused pickups p now, so
-  // the assignment step rarely waits for an A* (~0.9 ms on C3). Results-neutral: only WHEN a code is
-  // known changes. Pairs are not marked pending (like task chains).
-  auto predict = [&](uint32_t d) {
-    constexpr uint32_t KMAX = 8;
-    const uint32_t K = min(A.predict_k, KMAX);
-    const uint32_t dx = d % G.W, dy = d / G.W;
-    uint64_t best[KMAX];
-#pragma unroll
-    for (uint32_t i = 0; i < KMAX; ++i) best[i] = ~0ull;
-    for (uint32_t t = lane; t < A.m; t += 64u) {
-      if (A.used[t]) continue;
-      const uint32_t xy = A.pick_xy[t];
-      const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
-      uint64_t key = ((uint64_t)((dx > tx ? dx - tx : tx - dx) + (dy > ty ? dy - ty : ty - dy)) << 32) | t;
-#pragma unroll
-      for (uint32_t i = 0; i < KMAX; ++i) {  // sorted insert (keys are distinct: t is in them)
-        if (i < K && key < best[i]) {
-          const uint64_t x = best[i];
-          best[i] = key;
-          key = x;
-        }
-      }
-    }
-    for (uint32_t r = 0; r < K; ++r) {
-      uint64_t mn = best[0];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t y = __shfl_xor(mn, off, 64);
-        mn = y < mn ? y : mn;
-      }
-      if (mn == ~0ull) break;
-      if (best[0] == mn) {  // the winning lane pops its head
-#pragma unroll
-        for (uint32_t i = 0; i + 1 < KMAX; ++i) best[i] = best[i + 1];
-        best[KMAX - 1] = ~0ull;
-      }
-      const uint32_t p = A.pick[(uint32_t)mn];
-      if (p == d) continue;
-      const int32_t tab = A.goal_tab[p];
-      if (tab < 0) continue;
-      const uint8_t code = (uint8_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(d, tab) : 0u);
-      if (code == NH_UNKNOWN) publish_code(d, tab, resolve(d, p), false);
-    }
-  };
-  // one claimed entry of the needed (0) or speculative (1) queue: a pair, or a prediction job
-  auto serve = [&](int which, uint32_t idx) {
-    const uint32_t* e = reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : A.QS) + idx);
-    const uint32_t v = w_ld(e), goal = w_ld(e + 1);
-    const int32_t tab = (int32_t)w_ld(e + 2);
-    if (goal == PREDICT_JOB) {
-      cur_q = 3u;
-      predict(v);
-    } else {
-      cur_q = (uint32_t)which;
-      publish_code(v, tab, resolve(v, goal), false);
-    }
-  };
   const bool take_t = (blockIdx.x & A.tmask) == A.tmask;
   for (;;) {
     int which = -1;
@@ -1476,14 +1415,14 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
     idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
     // the entry was published by the planner's release of the head (or by the host before the
     // launch): read it past stale caches
-    if (which < 2) {
-      serve(which, idx);
-      continue;
-    }
-    const uint32_t* e = reinterpret_cast<const uint32_t*>(A.QT + idx);
+    const uint32_t* e = reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : A.QT) + idx);
     const uint32_t v = w_ld(e), goal = w_ld(e + 1);
     const int32_t tab = (int32_t)w_ld(e + 2);
-    cur_q = 2u;
+    cur_q = (uint32_t)which;
+    if (which < 2) {
+      publish_code(v, tab, resolve(v, goal), false);
+      continue;
+    }
     // task chain: the path an agent carrying this task walks from its pickup to the delivery
     // (every hop is get_path(cell, delivery)[1], tswap.rs:263-266): follow resolved codes and
     // resolve each unresolved hop in turn; stop at a pair someone else has queued, at a stay code,
@@ -1501,7 +1440,11 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
         w2 = __builtin_amdgcn_readfirstlane(w2);
         if (w2 < 0) break;
         i2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i2);
-        serve(w2, i2);
+        const uint32_t* e2 = reinterpret_cast<const uint32_t*>((w2 == 0 ? A.QN : A.QS) + i2);
+        const uint32_t v2 = w_ld(e2), g2 = w_ld(e2 + 1);
+        const int32_t t2 = (int32_t)w_ld(e2 + 2);
+        cur_q = (uint32_t)w2;
+        publish_code(v2, t2, resolve(v2, g2), false);
         cur_q = 2u;
       }
       uint8_t code = (uint8_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(c, tab) : 0u);

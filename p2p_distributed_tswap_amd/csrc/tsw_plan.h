@@ -88,7 +88,6 @@ struct PlanArgs {
   uint32_t coop;
   AstarQuery* QS;
   uint32_t qscap;
-  uint32_t predict_k;  // coop: at a pickup arrival queue a prediction job for the delivery cell (0: off)
   CoopCtl* cc;
   // host-visible (pinned, system-coherent) words: [0] set when the planner block is resident,
   // [1] abort (host watchdog: planner waits give up, workers exit), [2] planner heartbeat (timesteps)
@@ -123,15 +122,6 @@ struct WorkerArgs {
   uint32_t* epochs;   // per-slot tag epochs
   uint64_t* heaps;    // per-wave global heaps (tier 3), ghcap entries each
   uint32_t ghcap;
-  // assignment prediction jobs (speculative queue entries with goal == PREDICT_JOB): the K unused tasks
-  // whose pickups are nearest (Manhattan, then index) to the job's delivery cell, read from the
-  // planner's task arrays (possibly a little stale: a prediction only decides what gets resolved early)
-  const uint32_t* pick_xy;
-  const uint8_t* used;
-  const uint32_t* pick;
-  const int32_t* goal_tab;
-  uint32_t m;
-  uint32_t predict_k;
 };
 // Worker placement: per-wave LDS (heap, g-scores, free bitmap) sets the waves per CU. g-scores stay
 // in LDS (fastest per pop) unless that leaves < 3 waves per CU while many agents can need queries at

@@ -905,19 +905,6 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
                   S.G[ai] = ng;
                   S.GT[ai] = P.goal_tab[ng];
                   S.NHC[ai] = NHC_DIRTY;
-                  // coop: the workers predict the task this agent takes when it becomes idle at ng
-                  // (published with this step's PRE1 queue)
-                  if (P.coop && P.predict_k) {
-                    const uint32_t qi = atomicAdd(&s_q[1], 1u);
-                    if (qi < P.qscap) {
-                      AstarQuery q;
-                      q.v = ng;
-                      q.goal = PREDICT_JOB;
-                      q.tab = -1;
-                      q.out = qi;
-                      P.QS[qi] = q;
-                    }
-                  }
                 }
               } else if (st == ST_TO_DELIVERY) {
                 st = ST_IDLE;
