@@ -73,7 +73,6 @@ struct Tunables {
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
   bool task_chains = true;        // TSW_TASK_CHAINS=0: no task-chain jobs for the coop workers
-  bool walk_cache = true;         // TSW_WALK_CACHE=0: PRE1 walk-ahead re-walks every agent's path from its next cell each step
   bool chain_preempt = true;      // TSW_CHAIN_PREEMPT=0: chain workers finish a chain before serving queued pairs
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
 
@@ -111,7 +110,6 @@ struct Tunables {
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
     t.task_chains = num("TSW_TASK_CHAINS", 0, 1, 1) != 0;
     t.chain_preempt = num("TSW_CHAIN_PREEMPT", 0, 1, 1) != 0;
-    t.walk_cache = num("TSW_WALK_CACHE", 0, 1, 1) != 0;
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
     return t;
   }
@@ -205,7 +203,6 @@ struct tsw_ctx {
   // agents
   size_t acap = 0;
   uint32_t *d_v = nullptr, *d_g = nullptr, *d_cnt = nullptr, *d_succ = nullptr, *d_ap = nullptr;
-  uint32_t* d_wf = nullptr;  // k_plan walk-ahead frontier cache, 2 u32 per agent
   int32_t* d_gt = nullptr;
   uint8_t* d_dec = nullptr;
   uint8_t* d_onc = nullptr;
@@ -912,8 +909,7 @@ int ensure_agents(tsw_ctx* c, size_t n) {
     if (p) (void)hipFree(p);
   };
   fre(c->d_v); fre(c->d_g); fre(c->d_succ); fre(c->d_ap); fre(c->d_st); fre(c->d_task); fre(c->d_nhc);
-  fre(c->d_gt); fre(c->d_dec); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2); fre(c->d_wf);
-  HIPCHK(hipMalloc(&c->d_wf, cap * 8));
+  fre(c->d_gt); fre(c->d_dec); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
   HIPCHK(hipMalloc(&c->d_onc, cap));
   HIPCHK(hipMalloc(&c->d_candc, cap));
   HIPCHK(hipMalloc(&c->d_f1, (cap + 1) * 4));
@@ -976,10 +972,6 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.f1 = c->d_f1;
   P.f2 = c->d_f2;
   P.mk = c->d_ap;
-  // walk-ahead frontier cache: invalid at the start of every call (tables may have been evicted or
-  // their pending codes reset between calls); within a call codes only ever become resolved
-  P.wf = c->tun.walk_cache ? c->d_wf : nullptr;
-  if (P.wf) (void)hipMemsetAsync(c->d_wf, 0xFF, (size_t)n * 8u, c->s);
   P.occ = c->d_occ;
   P.mu = c->d_mu;
   P.has_dups = *c->h_dups;
@@ -1511,7 +1503,6 @@ void tsw_destroy(tsw_ctx* c) {
   fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf); fre(c->d_ovf2);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
   fre(c->d_gt); fre(c->d_dec); fre(c->d_mu); fre(c->d_dups); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
-  fre(c->d_wf);
   if (c->h_dups) (void)hipHostFree(c->h_dups);
   fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);

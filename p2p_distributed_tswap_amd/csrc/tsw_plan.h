@@ -67,7 +67,6 @@ struct PlanArgs {
   uint32_t* f1;   // pointer-doubling buffers, n + 1 entries each (global copy)
   uint32_t* f2;
   uint32_t* mk;   // per agent batch marks of the wave rules rounds (global copy, n + 1 entries)
-  uint32_t* wf;   // per agent walk-ahead frontier (cell, goal) of the last PRE1 walk, or null (no cache)
   uint32_t* occ;  // per cell occupancy
   uint64_t* mu;   // per cell round-tagged lowest undecided targeting agent (global copy)
   const uint32_t* pick_xy;

@@ -621,56 +621,6 @@ __device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, 
   return 0;
 }
 
-// walk_prefetch with the agent's last frontier cached (P.wf[2k] = cell, [2k+1] = goal): the walk of the
-// previous step stopped at x — its first unresolved cell (queued then, with the DAG past it) or
-// `hops` cells ahead. An agent only ever moves along its own next-hop codes, so while its goal is
-// unchanged x lies ahead of its next cell u on the same resolved path, dist(u) - dist(x) hops away
-// (K1 table): the walk resumes at x instead of re-reading every code from u, and a frontier that is
-// still pending is left alone (already queued with its DAG). Speculation only: which pairs are
-// queued, never what a step computes, depends on it.
-__device__ uint32_t walk_prefetch_cached(const PlanArgs& P, uint32_t* s_q, uint32_t k, uint32_t u, uint32_t g,
-                                         int32_t tab, uint32_t hops) {
-  uint32_t* wf = P.wf + 2u * k;
-  const uint32_t x = wf[0], xg = wf[1];
-  const uint16_t* dt = P.dist + (uint64_t)tab * P.nstride;
-  const uint8_t* ht = P.nh + (uint64_t)tab * P.nstride;
-  uint32_t cur = u, done = 0;
-  bool cached = false;
-  if (xg == g && x != NO_CELL) {
-    const uint32_t du = dt[u], dx = dt[x];
-    if (du != DIST_INF && dx <= du) {
-      done = du - dx;
-      if (done >= hops) return 0;  // the frontier is already `hops` cells ahead
-      cur = x;
-      cached = true;
-    }
-  }
-  const uint32_t budget = hops - done;
-  for (uint32_t h = 0; h < budget; ++h) {
-    if (cur == g) {
-      wf[0] = cur;
-      wf[1] = g;
-      return budget - h;
-    }
-    const uint8_t cu = ht[cur];
-    if (cu == NH_UNKNOWN || cu == NH_PENDING || cu == NH_PENDING_S) {
-      if (cu == NH_UNKNOWN) prefetch_pair(P, cur, g, tab, s_q);
-      if (P.dag_prefetch && !(cached && h == 0u && cu != NH_UNKNOWN)) dag_prefetch(P, s_q, cur, g, tab);
-      wf[0] = cur;
-      wf[1] = g;
-      return 0;
-    }
-    if (cu >= NH_STAY) {  // a stay code: nothing ahead
-      wf[0] = NO_CELL;
-      return 0;
-    }
-    cur = step_cell(cur, cu, P.W);
-  }
-  wf[0] = cur;
-  wf[1] = g;
-  return 0;
-}
-
 // Parallel: the next hop of every agent from the cell its resolved code points at (the pair the
 // movement phase or the next step reads after the agent moves, tswap.rs:263-273), walked `hops`
 // resolved cells ahead; speculative, bounded by half the queue like rules_prefetch.
@@ -707,9 +657,7 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
       if ((P.prefetch_ext & 1u) && P.dag_prefetch) dag_prefetch(P, s_q, S.V[k], S.G[k], tab);
       continue;
     }
-    const uint32_t u = step_cell(S.V[k], c, P.W);
-    const uint32_t left = P.wf ? walk_prefetch_cached(P, s_q, k, u, S.G[k], tab, hops)
-                               : walk_prefetch(P, s_q, u, S.G[k], tab, hops);
+    const uint32_t left = walk_prefetch(P, s_q, step_cell(S.V[k], c, P.W), S.G[k], tab, hops);
     if (left > 0u && dtab >= 0 && (P.prefetch_ext & 2u)) walk_prefetch(P, s_q, pc, dc, dtab, left);
   }
   __syncthreads();
