@@ -73,7 +73,6 @@ struct Tunables {
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
   bool task_chains = true;        // TSW_TASK_CHAINS=0: no task-chain jobs for the coop workers
-  bool far_queue = true;          // TSW_FAR_QUEUE=0: DAG prefetches share the near speculative queue
   bool chain_preempt = true;      // TSW_CHAIN_PREEMPT=0: chain workers finish a chain before serving queued pairs
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
 
@@ -111,7 +110,6 @@ struct Tunables {
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
     t.task_chains = num("TSW_TASK_CHAINS", 0, 1, 1) != 0;
     t.chain_preempt = num("TSW_CHAIN_PREEMPT", 0, 1, 1) != 0;
-    t.far_queue = num("TSW_FAR_QUEUE", 0, 1, 1) != 0;
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
     return t;
   }
@@ -1029,7 +1027,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
     P.QS = c->d_QS;
     P.qscap = (uint32_t)c->qscap;
     P.QF = c->d_QF;
-    P.qfcap = c->tun.far_queue ? (uint32_t)c->qfcap : 0u;
+    P.qfcap = (uint32_t)c->qfcap;
     P.cc = c->d_cc;
   }
   return P;

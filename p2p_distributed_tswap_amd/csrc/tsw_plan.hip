@@ -299,7 +299,6 @@ __device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uin
   uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
   if (*p != NH_UNKNOWN) return;
   if (P.coop) {
-    far = far && P.qfcap != 0u;  // qfcap 0 (TSW_FAR_QUEUE=0): one speculative queue
     const uint32_t qi = atomicAdd(&s_q[far ? 5 : 1], 1u);
     if (qi >= (far ? P.qfcap : P.qscap)) return;
     *p = NH_PENDING_S;
