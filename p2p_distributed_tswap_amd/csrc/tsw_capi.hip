@@ -185,8 +185,6 @@ struct tsw_ctx {
   CoopCtl* h_cc = nullptr;       // pinned
   AstarQuery* d_QS = nullptr;
   size_t qscap = 0;
-  AstarQuery* d_QF = nullptr;  // coop far speculative queue
-  size_t qfcap = 0;
   AstarQuery* d_QT = nullptr;    // task chains of the current plan (host-filled)
   size_t qtcap = 0;
   uint32_t qt_count = 0;
@@ -950,7 +948,6 @@ int ensure_coop(tsw_ctx* c, uint32_t n) {
   if (!c->d_QS) {
     HIPCHK(hipStreamSynchronize(c->s));
     HIPCHK(dgrow(c->d_QS, c->qscap, (size_t)1 << 20));
-    HIPCHK(dgrow(c->d_QF, c->qfcap, (size_t)1 << 20));
   }
   return TSW_OK;
 }
@@ -1026,8 +1023,6 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   if (P.coop) {
     P.QS = c->d_QS;
     P.qscap = (uint32_t)c->qscap;
-    P.QF = c->d_QF;
-    P.qfcap = (uint32_t)c->qfcap;
     P.cc = c->d_cc;
   }
   return P;
@@ -1061,7 +1056,6 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.cc = c->d_cc;
     W.QN = c->d_Q;
     W.QS = c->d_QS;
-    W.QF = c->d_QF;
     W.QT = c->d_QT;
     W.nh = c->d_nh;
     W.nstride = c->tstride;
@@ -1151,7 +1145,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       c->st.astar_queries += cc.worker_queries;
       if (cc.err) RET(TSW_EOVERFLOW, "K3 worker: A* heap overflow");
       // speculative pairs nobody claimed stay PENDING_S: back to UNKNOWN for later calls
-      if (cc.head_s > cc.claim_s || cc.head_f > cc.claim_f) {
+      if (cc.head_s > cc.claim_s) {
         HIPCHK(launch_reset_pending(c->d_nh, (uint64_t)c->tab_count * c->tstride, c->s));
         HIPCHK(hipStreamSynchronize(c->s));
       }
@@ -1512,7 +1506,7 @@ void tsw_destroy(tsw_ctx* c) {
   if (c->h_dups) (void)hipHostFree(c->h_dups);
   fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
-  fre(c->d_cc); fre(c->d_QS); fre(c->d_QF); fre(c->d_QT);
+  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->s2) (void)hipStreamDestroy(c->s2);

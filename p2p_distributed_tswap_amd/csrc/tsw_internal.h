@@ -62,8 +62,6 @@ struct CoopCtl {
   uint32_t claim_s, pad3[31];  // speculative queue: claimed
   uint32_t head_t, pad5[31];   // task-chain queue (filled by the host before the launch)
   uint32_t claim_t, pad6[31];  // task-chain queue: claimed
-  uint32_t head_f, pad8[31];   // far speculative queue (DAG prefetch, served after the near one): published
-  uint32_t claim_f, pad9[31];  // far speculative queue: claimed
   uint32_t pub, pad7[31];      // planner publish count: idle workers poll this one word
   uint32_t stop, alive, err, waits;  // planner finished / workers started / worker error bits / planner waits
   unsigned long long wait_ticks;     // planner time spent waiting on workers (100 MHz ticks)

@@ -1220,8 +1220,7 @@ __device__ __forceinline__ bool w_cas(uint32_t* p, uint32_t expect, uint32_t wan
                                               __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// lane 0: claim the next pair (0: needed queue, 1: speculative queue, 3: far speculative queue,
-// 2: task chain, -1: exit).
+// lane 0: claim the next pair (0: needed queue, 1: speculative queue, 2: task chain, -1: exit).
 // Task chains (long, lowest priority) only go to workers with take_t: the others stay free for the
 // pairs the planner needs or will need soon.
 __device__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags) {
@@ -1249,14 +1248,6 @@ __device__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint3
         if (w_cas(&cc->claim_s, cs, cs + 1u)) {
           *idx = cs;
           return 1;
-        }
-        continue;
-      }
-      const uint32_t hf = w_ld(&cc->head_f), cf = w_ld(&cc->claim_f);
-      if (cf < hf) {
-        if (w_cas(&cc->claim_f, cf, cf + 1u)) {
-          *idx = cf;
-          return 3;
         }
         continue;
       }
@@ -1298,7 +1289,7 @@ __device__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint3
   }
 }
 
-// lane 0, non-blocking: claim one pair of the needed or a speculative queue (0 / 1 / 3), else -1.
+// lane 0, non-blocking: claim one pair of the needed or the speculative queue (0 / 1), else -1.
 // A worker walking a task chain calls this between hops, so chains (lowest priority, up to ~100
 // A* each) never hold a worker while pairs the planner needs or will need soon are queued.
 __device__ int worker_try_claim(CoopCtl* cc, uint32_t* idx) {
@@ -1316,14 +1307,6 @@ __device__ int worker_try_claim(CoopCtl* cc, uint32_t* idx) {
       if (w_cas(&cc->claim_s, cs, cs + 1u)) {
         *idx = cs;
         return 1;
-      }
-      continue;
-    }
-    const uint32_t hf = w_ld(&cc->head_f), cf = w_ld(&cc->claim_f);
-    if (cf < hf) {
-      if (w_cas(&cc->claim_f, cf, cf + 1u)) {
-        *idx = cf;
-        return 3;
       }
       continue;
     }
@@ -1432,12 +1415,11 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
     idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
     // the entry was published by the planner's release of the head (or by the host before the
     // launch): read it past stale caches
-    const uint32_t* e = reinterpret_cast<const uint32_t*>(
-        (which == 0 ? A.QN : which == 1 ? A.QS : which == 3 ? A.QF : A.QT) + idx);
+    const uint32_t* e = reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : A.QT) + idx);
     const uint32_t v = w_ld(e), goal = w_ld(e + 1);
     const int32_t tab = (int32_t)w_ld(e + 2);
-    cur_q = which == 3 ? 1u : (uint32_t)which;
-    if (which != 2) {
+    cur_q = (uint32_t)which;
+    if (which < 2) {
       publish_code(v, tab, resolve(v, goal), false);
       continue;
     }
@@ -1458,10 +1440,10 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
         w2 = __builtin_amdgcn_readfirstlane(w2);
         if (w2 < 0) break;
         i2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i2);
-        const uint32_t* e2 = reinterpret_cast<const uint32_t*>((w2 == 0 ? A.QN : w2 == 1 ? A.QS : A.QF) + i2);
+        const uint32_t* e2 = reinterpret_cast<const uint32_t*>((w2 == 0 ? A.QN : A.QS) + i2);
         const uint32_t v2 = w_ld(e2), g2 = w_ld(e2 + 1);
         const int32_t t2 = (int32_t)w_ld(e2 + 2);
-        cur_q = w2 == 0 ? 0u : 1u;
+        cur_q = (uint32_t)w2;
         publish_code(v2, t2, resolve(v2, g2), false);
         cur_q = 2u;
       }

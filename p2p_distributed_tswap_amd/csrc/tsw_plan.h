@@ -88,8 +88,6 @@ struct PlanArgs {
   uint32_t coop;
   AstarQuery* QS;
   uint32_t qscap;
-  AstarQuery* QF;      // coop: far speculative queue (shortest-path DAG cells past a walk's frontier)
-  uint32_t qfcap;
   CoopCtl* cc;
   // host-visible (pinned, system-coherent) words: [0] set when the planner block is resident,
   // [1] abort (host watchdog: planner waits give up, workers exit), [2] planner heartbeat (timesteps)
@@ -111,7 +109,6 @@ struct WorkerArgs {
   CoopCtl* cc;
   const AstarQuery* QN;
   const AstarQuery* QS;
-  const AstarQuery* QF;  // far speculative pairs: claimed after the near speculative queue
   const AstarQuery* QT;  // task chains: (pickup, delivery) of every task, walked hop by hop
   uint8_t* nh;
   uint64_t nstride;

@@ -143,8 +143,7 @@ __device__ __forceinline__ uint32_t succ_of(const PlanArgs& P, const Arrays& S, 
 // pf (phase start, wide prefetch): rules_prefetch fused into the first pass — the pair (cell of
 // succ(k), goal of k) is the CANDC load itself, and k's own next pair is one more load — saving the
 // separate block-wide pass and its repeated table reads.
-__device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q,
-                                              bool far = false);
+__device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q);
 __device__ __forceinline__ bool spec_full(const PlanArgs& P, const uint32_t* s_q);
 __device__ void rules_init(const PlanArgs& P, const Arrays& S, uint32_t* pf = nullptr) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x, n = P.n;
@@ -284,30 +283,25 @@ __device__ __forceinline__ void enqueue_pair(const PlanArgs& P, uint32_t v, uint
 
 // speculative queue full (no more prefetches this launch)
 __device__ __forceinline__ bool spec_full(const PlanArgs& P, const uint32_t* s_q) {
-  // (coop: the near queue; the far one is checked where far pairs are queued)
   return P.coop ? *(volatile const uint32_t*)&s_q[1] >= P.qscap : *(volatile const uint32_t*)&s_q[0] >= P.qcap / 2u;
 }
 
 // A speculative prefetch. Exit mode: the slot is reserved by CAS only while the queue holds fewer
 // than qcap/2 pairs, so prefetches never take the room the needed pairs of an exit rely on. Coop
-// mode: its own queues, resolved by the workers after every needed pair — `far` pairs (the
-// shortest-path DAG past a walk's first unresolved cell, several steps away) in QF, served only when
-// the near queue QS (pairs a firing, a move or the next step reads) is empty, so a deep DAG backlog
-// never delays a pair needed sooner.
-__device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q,
-                                              bool far) {
+// mode: its own queue (QS), resolved by the workers after every needed pair.
+__device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q) {
   uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
   if (*p != NH_UNKNOWN) return;
   if (P.coop) {
-    const uint32_t qi = atomicAdd(&s_q[far ? 5 : 1], 1u);
-    if (qi >= (far ? P.qfcap : P.qscap)) return;
+    const uint32_t qi = atomicAdd(&s_q[1], 1u);
+    if (qi >= P.qscap) return;
     *p = NH_PENDING_S;
     AstarQuery q;
     q.v = v;
     q.goal = g;
     q.tab = tab;
     q.out = qi;
-    (far ? P.QF : P.QS)[qi] = q;
+    P.QS[qi] = q;
     return;
   }
   const uint32_t lim = P.qcap / 2u;
@@ -379,14 +373,12 @@ __device__ __forceinline__ bool plan_abort(const PlanArgs& P) {
 // thread 0: make every entry queued so far visible to the workers (caller: after a barrier). A publish
 // whose heads equal the last published ones is skipped: no entry and no PENDING mark was written since
 // (marks are only written with an entry), and the agent-scope release it would cost writes back this
-// XCD's L2. s_q[3] / s_q[4] / s_q[6] hold the last published heads (0 = the launch's zeroed CoopCtl).
+// XCD's L2. s_q[3] / s_q[4] hold the last published heads (0 = the launch's zeroed CoopCtl).
 __device__ __forceinline__ void coop_publish(const PlanArgs& P, uint32_t* s_q) {
-  const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap), hf = min(s_q[5], P.qfcap);
-  if (hn == s_q[3] && hs == s_q[4] && hf == s_q[6]) return;
+  const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap);
+  if (hn == s_q[3] && hs == s_q[4]) return;
   s_q[3] = hn;
   s_q[4] = hs;
-  s_q[6] = hf;
-  __hip_atomic_store(&P.cc->head_f, hf, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&P.cc->head_s, hs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&P.cc->head_n, hn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   // wake idle workers, which poll only this word (a plain agent-scope store of a new value)
@@ -602,7 +594,7 @@ __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint3
         if (!((nb >> d) & 1u)) continue;
         const uint32_t w = step_cell(x, d, P.W);
         if (w == g || (uint32_t)dt[w] + 1u != dx) continue;
-        if (ht[w] == NH_UNKNOWN) prefetch_pair(P, w, g, tab, s_q, lv > 0u);  // level 0: the next cells
+        if (ht[w] == NH_UNKNOWN) prefetch_pair(P, w, g, tab, s_q);
         add(w);
       }
     }
@@ -738,7 +730,7 @@ template <bool AG, bool OC, bool MUL>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[7], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
+  __shared__ uint32_t s_q[5], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[32], s_tlast, s_tp;
@@ -831,8 +823,6 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_q[2] = 0;  // publishes (coop mode)
     s_q[3] = 0;  // last published needed / speculative heads (coop mode)
     s_q[4] = 0;
-    s_q[5] = 0;  // far speculative queue (coop mode)
-    s_q[6] = 0;  // its last published head
     for (int k = 0; k < 32; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
