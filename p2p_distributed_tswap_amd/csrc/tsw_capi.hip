@@ -73,6 +73,7 @@ struct Tunables {
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
   bool coop = true;               // TSW_COOP=0: K3 as host-launched passes at planner exits (round-1 mode)
   bool task_chains = true;        // TSW_TASK_CHAINS=0: no task-chain jobs for the coop workers
+  bool avoid_xcc = true;          // TSW_WORKER_AVOID_XCD=0: coop workers also run on the planner's XCD
   bool chain_preempt = true;      // TSW_CHAIN_PREEMPT=0: chain workers finish a chain before serving queued pairs
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
 
@@ -110,6 +111,7 @@ struct Tunables {
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
     t.task_chains = num("TSW_TASK_CHAINS", 0, 1, 1) != 0;
     t.chain_preempt = num("TSW_CHAIN_PREEMPT", 0, 1, 1) != 0;
+    t.avoid_xcc = num("TSW_WORKER_AVOID_XCD", 0, 1, 1) != 0;
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
     return t;
   }
@@ -1064,6 +1066,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     // are larger), the rest stay free for the pairs the planner waits on
     W.tmask = P.n > 2000u ? 3u : 1u;
     W.preempt = c->tun.chain_preempt ? 1u : 0u;
+    W.avoid_xcc = c->tun.avoid_xcc ? 1u : 0u;
     W.hflags = c->d_flags;
     W.gs_all = c->d_gs;
     W.epochs = c->d_epochs;

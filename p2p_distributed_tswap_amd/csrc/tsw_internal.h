@@ -63,6 +63,7 @@ struct CoopCtl {
   uint32_t head_t, pad5[31];   // task-chain queue (filled by the host before the launch)
   uint32_t claim_t, pad6[31];  // task-chain queue: claimed
   uint32_t pub, pad7[31];      // planner publish count: idle workers poll this one word
+  uint32_t planner_xcc, pad8[31];  // 1 + XCD of the planner block (0: unknown), written before it signals residency
   uint32_t stop, alive, err, waits;  // planner finished / workers started / worker error bits / planner waits
   unsigned long long wait_ticks;     // planner time spent waiting on workers (100 MHz ticks)
   unsigned long long worker_queries; // queries resolved by workers

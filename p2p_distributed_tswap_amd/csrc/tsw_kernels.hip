@@ -1346,6 +1346,12 @@ __global__ void __launch_bounds__(64) k_astar_worker(WorkerArgs A) {
   uint32_t* GSg = A.gs_all + (uint64_t)blockIdx.x * ncell;
   uint64_t* Hg = A.heaps + (uint64_t)blockIdx.x * A.ghcap;
   uint32_t ep = A.epochs[blockIdx.x], epl = 0;
+  // a worker on the planner's XCD leaves at once: the planner's agent arrays, occupancy and table
+  // lines then share that XCD's 4 MB L2 with nobody's g-score slots (wave-uniform exit, before `alive`)
+  if (A.avoid_xcc) {
+    const uint32_t px = w_ld(&A.cc->planner_xcc);
+    if (px != 0u && px - 1u == (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20)) return;
+  }
   __syncthreads();
   if (lane == 0) __hip_atomic_fetch_add(&A.cc->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // exact A* for (v, goal): tier 1 LDS heap + LDS (or global) g-scores, tier 2 global u32

@@ -122,6 +122,7 @@ struct WorkerArgs {
   uint32_t* epochs;   // per-slot tag epochs
   uint64_t* heaps;    // per-wave global heaps (tier 3), ghcap entries each
   uint32_t ghcap;
+  uint32_t avoid_xcc;  // workers placed on the planner's XCD exit at once (its L2 stays the planner's)
 };
 // Worker placement: per-wave LDS (heap, g-scores, free bitmap) sets the waves per CU. g-scores stay
 // in LDS (fastest per pop) unless that leaves < 3 waves per CU while many agents can need queries at

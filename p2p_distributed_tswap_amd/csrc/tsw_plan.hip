@@ -828,7 +828,13 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     s_tsec = 7;  // entry / copy-in
     // coop mode: tell the host the planner is resident, so the workers it launches next cannot
     // take the CUs this block needs
-    if (P.hflags) __hip_atomic_store(&P.hflags[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (P.hflags) {
+      // the XCD this block runs on: workers the host launches next skip it (TSW_WORKER_AVOID_XCD)
+      if (P.coop)
+        __hip_atomic_store(&P.cc->planner_xcc, 1u + (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&P.hflags[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   __syncthreads();
   if (s_ctl.section == SEC_RULES || s_ctl.section == SEC_MOVE) {
