@@ -100,13 +100,28 @@ struct Arrays {
   uint8_t* USED;
 };
 
+// Next-hop code of (v, goal slot tab). A plain load may return a stale PENDING from this XCD's L2
+// after a worker has stored the code (coop mode): then the word is read again at agent scope, so a
+// code that is already known does not send the planner through a refresh pass and a wait. Codes never
+// change once written, so either read is exact.
+__device__ __forceinline__ uint8_t nh_code(const PlanArgs& P, int32_t tab, uint32_t v) {
+  const uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
+  uint8_t c = *p;
+  if (P.coop && (c == NH_PENDING || c == NH_PENDING_S)) {
+    const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c = (uint8_t)(w >> (8u * (uint32_t)((uintptr_t)p & 3u)));
+  }
+  return c;
+}
+
 // next-hop code of agent k for its current (v, g); -1 unresolved, -2 goal has no table
 __device__ __forceinline__ int lookup_code(const PlanArgs& P, const Arrays& S, uint32_t k) {
   const uint8_t c = S.NHC[k];
   if (c <= NH_STAY) return c;
   const int32_t tab = S.GT[k];
   if (tab < 0) return -2;
-  const uint8_t code = P.nh[(uint64_t)tab * P.nstride + S.V[k]];
+  const uint8_t code = nh_code(P, tab, S.V[k]);
   if (code <= NH_STAY) {
     S.NHC[k] = code;
     return code;
@@ -333,7 +348,7 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
       atomicOr(&P.ctl->err, ERR_NO_TABLE);
       continue;
     }
-    const uint8_t code = P.nh[(uint64_t)tab * P.nstride + v];
+    const uint8_t code = nh_code(P, tab, v);
     if (code <= NH_STAY) {
       S.NHC[k] = code;
     } else {
@@ -1059,7 +1074,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
         const uint32_t candc = S.CANDC[b];
         if (vs == gs) {  // rule 3: goal swap (tswap.rs:198-202)
           uint32_t code = candc;
-          if (code > NH_STAY && tb >= 0) code = P.nh[(uint64_t)tb * P.nstride + vs];  // s's new goal is gb
+          if (code > NH_STAY && tb >= 0) code = nh_code(P, tb, vs);  // s's new goal is gb
           S.G[b] = gs;
           S.GT[b] = ts;
           S.G[s] = gb;
@@ -1165,7 +1180,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
           uint8_t code = S.CANDC[pa];
           if (code > NH_STAY) {
             const int32_t tab = S.GT[a];
-            code = tab >= 0 ? P.nh[(uint64_t)tab * P.nstride + S.V[a]] : NH_UNKNOWN;
+            code = tab >= 0 ? nh_code(P, tab, S.V[a]) : NH_UNKNOWN;
           }
           if (code <= NH_STAY) S.NHC[a] = code;
           else bad = true;
@@ -1223,7 +1238,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
               const uint32_t vk = S.V[k];
               uint32_t code = S.CANDC[k];
               bool ok = p_vs == p_gs && vk != p_gs;  // rule 3 without a shared start cell
-              if (ok && code > NH_STAY) code = p_tk >= 0 ? P.nh[(uint64_t)p_tk * P.nstride + p_vs] : NH_UNKNOWN;
+              if (ok && code > NH_STAY) code = p_tk >= 0 ? nh_code(P, p_tk, p_vs) : NH_UNKNOWN;
               ok = ok && code <= NH_STAY;
               p_code = code;
               uint32_t ns = SUCC_TERM;
