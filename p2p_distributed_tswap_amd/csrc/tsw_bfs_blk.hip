@@ -111,12 +111,12 @@ __host__ __device__ __forceinline__ uint32_t blk_shared_u64(uint32_t nbp) {
 
 // WLS: the west-step blocks WL live in the wave's LDS (after V) instead of global scratch — no
 // memory-side atomics, at the cost of ~nbp*8 more LDS bytes per goal in flight.
-// PAIR: each 32-lane half of a wave runs its own goal (two goals per wave, in lockstep: both
-// halves start together, run levels until both BFS are done, then decode together). A level's
-// instruction stream then advances two goals; the level loop is bound by its dependent latency
-// chain (~3,250 cycles per level at 3 waves per SIMD for ~270 instructions), so halving the
-// instructions per goal-level costs little latency. LDS per goal is unchanged (goal slots, not
-// waves, are what LDS bounds); the global scratch (WL, anchors, list overflow) is per goal slot.
+// PAIR (TSW_BFS_PAIR=1, A/B variant): each 32-lane half of a wave runs its own goal (two goals per
+// wave, in lockstep: both halves start together, run levels until both BFS are done, then decode
+// together), so one level's instruction stream advances two goals at the same LDS per goal; the
+// global scratch (WL, anchors, list overflow) is per goal slot. Measured slower on den520d (3.66 vs
+// 2.68 ms per 10k goals): per-half state moves to VGPRs and the larger of two fronts needs more
+// chunk passes, lengthening the dependent level chain that bounds the loop.
 template <bool WLS, bool PAIR>
 __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
   extern __shared__ __align__(16) uint64_t smem64[];
