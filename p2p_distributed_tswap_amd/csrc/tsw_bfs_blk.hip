@@ -253,13 +253,13 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     };
     // run-start anchors among this half's new cells (block's run starts numbered in block order)
-    auto anchors2 = [&](uint32_t p, uint32_t nw, uint32_t f0, uint32_t fw, uint32_t lvl) {
+    auto anchors2 = [&](uint32_t p, uint32_t nw, uint32_t f0, uint32_t fw, uint32_t lvl, uint32_t abp) {
       const uint32_t bx = p - __umulhi(p, A.bp_magic) * Bp;
       const uint32_t wf = ((f0 << 1) & ~C0) | ((bx & 3u) ? ((fw >> 7) & C0) : 0u);
       const uint32_t rs = f0 & ~wf;
       const uint32_t below = __popc(partner(rs));  // the low half's run starts precede ours
       uint32_t rsn = (A.dbg & 4u) ? 0u : nw & rs;
-      const uint32_t base = AB[p] + (h ? below : 0u);
+      const uint32_t base = abp + (h ? below : 0u);
       while (rsn) {
         const uint32_t bb = (uint32_t)__builtin_ctz(rsn);
         anch[base + __popc(rs & ((1u << bb) - 1u))] = (uint16_t)lvl;
@@ -270,9 +270,11 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
     // lvl + 1 — self (either half, or across the halves), W / E (either half), N (row 0, even
     // lane), S (row 7, odd lane); dedup by test-and-set on the next level's flags, appends by
     // ballot + mbcnt. Even lanes own (self, W, N), odd lanes (E, S).
+    // `overlap` runs after the three returning dedup atomics are issued and before their results are
+    // used (the run-start anchor stores), so it hides under their LDS latency
     auto push2 = [&](uint32_t p, uint32_t nw, uint32_t vv, uint32_t f0, uint32_t fw, uint32_t fe, uint32_t fx,
                     uint32_t fp, uint32_t vw, uint32_t ve, uint32_t vx, uint32_t vp, uint32_t* Fn, uint16_t* Ln,
-                    uint16_t* On) {
+                    uint16_t* On, auto&& overlap) {
       const uint32_t in = ((nw << 1) & ~C0) | ((nw >> 1) & ~C7) | (nw << 8) | (nw >> 8);
       const uint32_t cross = h ? (nw << 24) : (nw >> 24);  // row 4 -> row 3 / row 3 -> row 4
       const bool s_self = ((in & f0 & ~vv) | (cross & fp & ~vp)) != 0u;
@@ -292,6 +294,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         return atomicOr(&Fn[w ? (t & kmask) : lane], m) & m;
       };
       const uint32_t o0 = tas2(w0, t0), o1 = tas2(w1, t1), o2 = tas2(w2, t2);
+      overlap();
       w0 = w0 && !o0;
       w1 = w1 && !o1;
       w2 = w2 && !o2;
@@ -375,6 +378,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         const uint32_t ox = h ? 2u * (p + Bp) : 2u * (p - Bp) + 1u;  // vertical neighbour dword
         const uint32_t v0 = V32[o], vw = V32[o - 2u], ve = V32[o + 2u], vx = V32[ox];
         const uint32_t f0 = FR32[o], fw = FR32[o - 2u], fe = FR32[o + 2u], fx = FR32[ox];
+        const uint32_t abp = AB[p];
         const uint32_t vp = partner(v0), fp = partner(f0);
         const uint32_t a = v0 & psrc2, aw = vw & psrc2, ae = ve & psrc2, ax = vx & psrc2, ap = vp & psrc2;
         const uint32_t up_in = h ? (ap >> 24) : (ax >> 24);   // row above the half's top row
@@ -391,8 +395,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         }
         const uint32_t nwp = partner(nw);
         bad |= act && (nw | nwp) == 0u;  // entries must gain a cell
-        anchors2(p, nw, f0, fw, lvl);
-        push2(p, nw, vv, f0, fw, fe, fx, fp, vw, ve, vx, vp, Fn, Ln, On);
+        push2(p, nw, vv, f0, fw, fe, fx, fp, vw, ve, vx, vp, Fn, Ln, On, [&]() { anchors2(p, nw, f0, fw, lvl, abp); });
         ++n_chunk;
       };
       // path choice and trip counts are wave-uniform (PAIR: over both halves' lists)
