@@ -83,17 +83,30 @@ typedef struct {
     uint8_t pad[3];
 } tsw_rec;
 
+/* Context options. Every option is results-neutral: plans, tables and next hops are bit-identical
+ * whatever is set here; only time and memory change. The production library reads nothing from the
+ * environment — these fields are its whole configuration surface. */
 typedef struct {
-    int32_t device;              /* HIP device ordinal (default 0)             */
-    uint32_t flags;              /* TSW_F_* below                              */
-    uint64_t table_budget_bytes; /* cap for distance+next-hop tables (0=auto)  */
+    int32_t device;              /* HIP device ordinal (default 0)                                  */
+    uint32_t flags;              /* TSW_F_* below                                                   */
+    uint64_t table_budget_bytes; /* cap for distance+next-hop tables, 3 B per cell per goal
+                                    (0 = half of the device's free memory at tsw_create)            */
+    uint32_t watchdog_ms;        /* plan calls: if the planner records no timestep for this long,
+                                    the call finishes in exit mode (0 = 10000)                      */
+    uint32_t reserved;
 } tsw_opts;
 
 /* Resolve every multi-candidate next hop of every table eagerly (one big
- * batched A* pass right after the BFS tables) instead of lazily per step. */
+ * batched A* pass right after the BFS tables) instead of lazily per step.
+ * (default: eager when the grid has <= 4096 cells and the new tables hold <= 8M cells) */
 #define TSW_F_EAGER_NEXTHOP 1u
 /* Never eager (lazy only), even when the auto policy would pick eager. */
 #define TSW_F_LAZY_NEXTHOP 2u
+/* Lazy next hops without concurrent K3 workers: the plan kernel exits to the host whenever a step
+ * needs unresolved next hops and is relaunched after a batched A* pass ("exit mode"). Default
+ * (coop mode): the plan dispatch also runs exact-A* worker waves on the other CUs, which the planner
+ * feeds through device queues and waits on only when a step needs a code. */
+#define TSW_F_EXIT_MODE 4u
 
 /* Replaces the graph build of tswap_mapd (tswap.rs:44-77) and of the
  * centralized manager (bin/centralized/manager.rs:503-535): uploads the grid
@@ -216,6 +229,11 @@ typedef struct {
     uint64_t relabels_full, relabels_inc;
     uint64_t move_rounds;       /* decidability rounds run by the movement phase */
     uint32_t plan_block;        /* workgroup size of the last plan kernel launch */
+    uint32_t coop_workers;      /* K3 worker waves in the last coop plan dispatch */
+    /* coop mode: wall time the workers spent inside A*, summed over worker waves (wave-ms), by queue:
+     * [0] needed pairs, [1] speculative prefetches, [2] task chains */
+    double coop_worker_busy_ms[3];
+    uint64_t watchdog_fires;    /* plan calls the host watchdog moved to exit mode */
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

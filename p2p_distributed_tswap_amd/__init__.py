@@ -30,9 +30,12 @@ __all__ = [
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtswap_hip.so")
+# diagnostic build (-DTSW_DIAG): the same kernels plus the TSW_* environment knobs (kernel A/B variants,
+# instrumentation). Tests of the A/B variants and measurement scripts only; products load LIB_PATH.
+DIAG_LIB_PATH = os.path.join(_HERE, "libtswap_hip_diag.so")
 
 TSW_OK, TSW_EINVAL, TSW_ENOMEM, TSW_EHIP, TSW_EOVERFLOW = 0, -22, -12, -5, -75
-TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP = 1, 2
+TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP, TSW_F_EXIT_MODE = 1, 2, 4
 # TswapAction (bin/decentralized/agent.rs:321-326), include/tswap.h TSW_ACT_*
 TSW_ACT_MOVE, TSW_ACT_GOAL_SWAP, TSW_ACT_ROTATION, TSW_ACT_WAIT = 0, 1, 2, 3
 DIST_INF = 0xFFFF
@@ -76,7 +79,8 @@ class _Rec(ctypes.Structure):
 
 class _Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("table_budget_bytes", ctypes.c_uint64)]
+                ("table_budget_bytes", ctypes.c_uint64), ("watchdog_ms", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):
@@ -92,6 +96,8 @@ class Stats(ctypes.Structure):
         ("coop_wait_sec_ms", ctypes.c_double * 8), ("coop_waits_sec", ctypes.c_uint64 * 8),
         ("relabels_full", ctypes.c_uint64), ("relabels_inc", ctypes.c_uint64),
         ("move_rounds", ctypes.c_uint64), ("plan_block", ctypes.c_uint32),
+        ("coop_workers", ctypes.c_uint32), ("coop_worker_busy_ms", ctypes.c_double * 3),
+        ("watchdog_fires", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -100,6 +106,7 @@ class Stats(ctypes.Structure):
         d["plan_exits"] = list(self.plan_exits)
         d["coop_wait_sec_ms"] = list(self.coop_wait_sec_ms)
         d["coop_waits_sec"] = list(self.coop_waits_sec)
+        d["coop_worker_busy_ms"] = list(self.coop_worker_busy_ms)
         return d
 
 
@@ -111,14 +118,13 @@ EXPORTED_SYMBOLS = (
     "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing", "tsw_probe_round_floors",
 )
 
-_lib = None
+_libs = {}
 
 
 def load_library(path: str = LIB_PATH):
     """Load libtswap_hip.so (built by __graft_entry__.build()). Raises if absent."""
-    global _lib
-    if _lib is not None:
-        return _lib
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise TswapError(TSW_EHIP, f"HIP library not built: {path} (run __graft_entry__.build())")
     lib = ctypes.CDLL(path)
@@ -153,7 +159,7 @@ def load_library(path: str = LIB_PATH):
                  "tsw_next_hop_tables_device", "tsw_import_next_hops_device", "tsw_get_stats", "tsw_reset_stats",
                  "tsw_set_timing", "tsw_probe_round_floors"):
         getattr(lib, name).restype = ctypes.c_int
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
@@ -181,11 +187,14 @@ def _u32p(a):
 class Planner:
     """One device context (tsw_ctx) bound to a grid."""
 
-    def __init__(self, grid, device: int = 0, flags: int = 0, table_budget_bytes: int = 0):
-        self._lib = load_library()
+    def __init__(self, grid, device: int = 0, flags: int = 0, table_budget_bytes: int = 0, watchdog_ms: int = 0,
+                 diag: bool = False):
+        """flags: TSW_F_*; watchdog_ms: tsw_opts.watchdog_ms (0 = 10 s); diag: bind the diagnostic
+        build (reads the TSW_* environment knobs at creation) instead of the production library."""
+        self._lib = load_library(DIAG_LIB_PATH if diag else LIB_PATH)
         cells, w, h = grid_to_bytes(grid)
         self.w, self.h = int(w), int(h)
-        opts = _Opts(device, flags, table_budget_bytes)
+        opts = _Opts(device, flags, table_budget_bytes, watchdog_ms, 0)
         ptr = self._lib.tsw_create(cells.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), w, h,
                                    ctypes.byref(opts))
         if not ptr:

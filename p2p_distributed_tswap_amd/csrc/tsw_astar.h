@@ -1,0 +1,512 @@
+// tsw_astar.h — exact A* next hop (get_path, tswap.rs:288-390) as device functions shared by
+// the K3 kernels (tsw_kernels.hip) and the coop workers inside the plan dispatch (tsw_plan.hip).
+// Rust std BinaryHeap semantics restated (push = sift_up; pop = swap last into the root,
+// sift_down_to_bottom, sift_up), ordered by AstarNode::cmp (tswap.rs:314-321). gfx950 only.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "tsw_internal.h"
+
+namespace tsw {
+
+// neighbour directions S,E,N,W = (0,+1),(+1,0),(0,-1),(-1,0): tswap.rs:62
+__device__ __forceinline__ uint32_t step_cell(uint32_t c, uint32_t code, uint32_t W) {
+  switch (code) {
+    case 0: return c + W;
+    case 1: return c + 1;
+    case 2: return c - W;
+    case 3: return c - 1;
+    default: return c;
+  }
+}
+
+// Unreachable-goal fallback of get_path (tswap.rs:378-389): the first
+// neighbour (S,E,N,W order) strictly closer in Manhattan distance; every
+// improving neighbour is exactly 1 closer, so "first improving" == argmin.
+__device__ __forceinline__ uint8_t fallback_code(uint8_t m, uint32_t x, uint32_t y, uint32_t gx,
+                                                 uint32_t gy) {
+  if ((m & 1) && gy > y) return 0;
+  if ((m & 2) && gx > x) return 1;
+  if ((m & 4) && gy < y) return 2;
+  if ((m & 8) && gx < x) return 3;
+  return NH_STAY;
+}
+
+// Next-hop classification from a distance table (any address space).
+__device__ __forceinline__ uint8_t classify_cell(const uint16_t* D, uint32_t c, uint8_t m,
+                                                 uint32_t W, uint32_t goal, uint32_t gx,
+                                                 uint32_t gy) {
+  if (!(m & NB_FREE)) return NH_UNKNOWN;
+  if (c == goal) return NH_STAY;
+  const uint16_t d = D[c];
+  if (d == DIST_INF) return fallback_code(m, c % W, c / W, gx, gy);
+  const uint16_t want = (uint16_t)(d - 1);
+  uint32_t cntc = 0, best = 0;
+#pragma unroll
+  for (uint32_t dir = 0; dir < 4; ++dir) {
+    if (m & (1u << dir)) {
+      if (D[step_cell(c, dir, W)] == want) {
+        ++cntc;
+        best = dir;
+      }
+    }
+  }
+  return cntc == 1 ? (uint8_t)best : NH_UNKNOWN;
+}
+
+__device__ __forceinline__ uint32_t fast_div(uint32_t a, uint32_t b, float inv) {
+  uint32_t q = (uint32_t)((float)a * inv);
+  while (q * b > a) --q;
+  while ((q + 1) * b <= a) ++q;
+  return q;
+}
+
+// ----------------------------------------------------------------------------
+// K3: exact A* next hop, one query per lane.
+// Heap entry: f:21 | g:21 | x:11 | y:11; Rust "a <= b" == key(a) >= key(b).
+// g_score word per cell: tag:10 | label:2 | g:20 where label = direction of
+// path[1] from the start. label(child) = dir if parent is the start, else
+// label(parent) at relaxation time; with a consistent heuristic (Manhattan on
+// a 4-grid) a node's g, came_from and hence label are final when it is first
+// popped, and stale pops relax nothing, so label(goal) at the goal's pop ==
+// the direction of path[1] of the reference's came_from chain (tswap.rs:344-355).
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mk_entry(uint32_t f, uint32_t g, uint32_t x, uint32_t y) {
+  return ((uint64_t)f << 43) | ((uint64_t)g << 22) | ((uint64_t)x << 11) | (uint64_t)y;
+}
+__device__ __forceinline__ uint64_t ekey(uint64_t e) { return e >> KEY_SHIFT; }
+
+// BinaryHeap::sift_up(start = 0, pos) with `elem` in the hole.
+__device__ __forceinline__ void heap_sift_up(uint64_t* Hp, uint32_t pos, uint64_t elem) {
+  const uint64_t k = ekey(elem);
+  while (pos > 0) {
+    const uint32_t parent = (pos - 1u) >> 1;
+    const uint64_t pe = Hp[parent];
+    if (k >= ekey(pe)) break;  // elem <= parent
+    Hp[pos] = pe;
+    pos = parent;
+  }
+  Hp[pos] = elem;
+}
+
+// BinaryHeap::pop with sift_down_to_bottom(0).
+__device__ __forceinline__ uint64_t heap_pop(uint64_t* Hp, uint32_t& len) {
+  const uint32_t end = --len;
+  const uint64_t last = Hp[end];
+  if (end == 0) return last;
+  const uint64_t top = Hp[0];
+  uint32_t pos = 0, child = 1;
+  while (child + 1u < end) {  // child <= end - 2
+    uint64_t l = Hp[child];
+    const uint64_t r = Hp[child + 1];
+    if (ekey(l) >= ekey(r)) {  // left <= right: take the right child
+      ++child;
+      l = r;
+    }
+    Hp[pos] = l;
+    pos = child;
+    child = 2u * pos + 1u;
+  }
+  if (child == end - 1u) {
+    Hp[pos] = Hp[child];
+    pos = child;
+  }
+  heap_sift_up(Hp, pos, last);
+  return top;
+}
+
+// err == nullptr: a heap overflow returns NH_UNKNOWN with *len_out = -2 (caller re-queues the
+// query to a larger heap) instead of raising ERR_HEAP_OVERFLOW.
+__device__ __forceinline__ uint8_t astar_one(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag, uint64_t* Hp,
+                                             uint32_t hcap, uint32_t* GS, int32_t* len_out, uint32_t* err) {
+  const uint32_t W = G.W;
+  const uint32_t vx = v % W, vy = v / W, gx = goal % W, gy = goal / W;
+  if (v == goal) {
+    *len_out = 1;
+    return NH_STAY;
+  }
+  const uint32_t tagw = tag << 22;
+  uint32_t len = 0;
+  GS[v] = tagw;
+  {
+    const uint32_t h0 = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
+    Hp[0] = mk_entry(h0, 0, vx, vy);
+    len = 1;
+  }
+  while (len > 0) {
+    const uint64_t e = heap_pop(Hp, len);
+    const uint32_t cx = (uint32_t)(e >> 11) & 0x7FFu, cy = (uint32_t)e & 0x7FFu;
+    const uint32_t cg = (uint32_t)(e >> 22) & 0x1FFFFFu;
+    const uint32_t c = cy * W + cx;
+    if (c == goal) {
+      *len_out = (int32_t)cg + 1;
+      return (uint8_t)((GS[goal] >> 20) & 3u);
+    }
+    const uint8_t m = G.nbmask[c];
+    const uint32_t labc = (GS[c] >> 20) & 3u;
+    const uint32_t tg = cg + 1u;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+      if (!(m & (1u << d))) continue;
+      const uint32_t nx = d == 1 ? cx + 1 : (d == 3 ? cx - 1 : cx);
+      const uint32_t ny = d == 0 ? cy + 1 : (d == 2 ? cy - 1 : cy);
+      const uint32_t nc = ny * W + nx;
+      const uint32_t old = GS[nc];
+      const uint32_t oldg = ((old & 0xFFC00000u) == tagw) ? (old & GS_G_MASK) : 0xFFFFFFFFu;
+      if (tg < oldg) {
+        const uint32_t lab = cg == 0 ? d : labc;
+        GS[nc] = tagw | (lab << 20) | tg;
+        if (len >= hcap) {
+          if (err) atomicOr(err, ERR_HEAP_OVERFLOW);
+          *len_out = err ? -1 : -2;
+          return NH_UNKNOWN;
+        }
+        const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
+        heap_sift_up(Hp, len, mk_entry(tg + h, tg, nx, ny));
+        ++len;
+      }
+    }
+  }
+  *len_out = 2;
+  return fallback_code(G.nbmask[v], vx, vy, gx, gy);
+}
+
+// ----------------------------------------------------------------------------
+// Single-lane A* core for k_astar_wave. A lone lane is instruction-bound, so the heap entry
+// keeps its ORDER KEY in the high dword: (f << 15 | g) << 32 | x << 16 | y — one 32-bit
+// compare per sift step and no division to recover (x, y). Same order as mk_entry's key
+// (f, then g; cell bits never compared). f >= 2^17 or g >= 2^15 hands the query off (-2).
+// GSM 0/1: u32 tag | label | g words (global slot / LDS); GSM 2: byte words as astar_one_b8.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t hk(uint64_t e) { return (uint32_t)(e >> 32); }
+
+__device__ __forceinline__ void hk_sift_up(uint64_t* Hp, uint32_t pos, uint64_t elem) {
+  const uint32_t k = hk(elem);
+  while (pos > 0) {
+    const uint32_t parent = (pos - 1u) >> 1;
+    const uint64_t pe = Hp[parent];
+    if (k >= hk(pe)) break;  // elem <= parent
+    Hp[pos] = pe;
+    pos = parent;
+  }
+  Hp[pos] = elem;
+}
+
+__device__ __forceinline__ uint64_t hk_pop(uint64_t* Hp, uint32_t& len) {
+  const uint32_t end = --len;
+  const uint64_t last = Hp[end];
+  if (end == 0) return last;
+  const uint64_t top = Hp[0];
+  uint32_t pos = 0, child = 1;
+  while (child + 1u < end) {
+    uint64_t l = Hp[child];
+    const uint64_t r = Hp[child + 1];
+    if (hk(l) >= hk(r)) {  // left <= right: take the right child
+      ++child;
+      l = r;
+    }
+    Hp[pos] = l;
+    pos = child;
+    child = 2u * pos + 1u;
+  }
+  if (child == end - 1u) {
+    Hp[pos] = Hp[child];
+    pos = child;
+  }
+  hk_sift_up(Hp, pos, last);
+  return top;
+}
+
+template <int GSM>
+__device__ __forceinline__ uint8_t astar_wave_core(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag,
+                                                   uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
+                                                   int32_t* len_out) {
+  const uint32_t W = G.W;
+  const uint32_t vy = v / W, vx = v - vy * W, gy = goal / W, gx = goal - gy * W;
+  if (v == goal) {
+    *len_out = 1;
+    return NH_STAY;
+  }
+  const uint32_t tagw = tag << 22;
+  if constexpr (GSM == 2) GB[v] = 0x80u;
+  else GS[v] = tagw;
+  const uint32_t h0 = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
+  if (h0 >= (1u << 17)) {
+    *len_out = -2;
+    return NH_UNKNOWN;
+  }
+  Hp[0] = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
+  uint32_t len = 1;
+  while (len > 0) {
+    const uint64_t e = hk_pop(Hp, len);
+    const uint32_t cx = (uint32_t)(e >> 16) & 0xFFFFu, cy = (uint32_t)e & 0xFFFFu;
+    const uint32_t cg = hk(e) & 0x7FFFu;
+    const uint32_t c = cy * W + cx;
+    if (c == goal) {
+      *len_out = (int32_t)cg + 1;
+      if constexpr (GSM == 2) return (uint8_t)((GB[goal] >> 5) & 3u);
+      else return (uint8_t)((GS[goal] >> 20) & 3u);
+    }
+    const uint32_t m = G.nbmask[c];
+    uint32_t labc;
+    if constexpr (GSM == 2) labc = (GB[c] >> 5) & 3u;
+    else labc = (GS[c] >> 20) & 3u;
+    const uint32_t tg = cg + 1u;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+      if (!(m & (1u << d))) continue;
+      const uint32_t nx = d == 1 ? cx + 1 : (d == 3 ? cx - 1 : cx);
+      const uint32_t ny = d == 0 ? cy + 1 : (d == 2 ? cy - 1 : cy);
+      const uint32_t nc = ny * W + nx;
+      uint32_t oldg;
+      uint32_t man = 0;
+      if constexpr (GSM == 2) {
+        man = (nx > vx ? nx - vx : vx - nx) + (ny > vy ? ny - vy : vy - ny);
+        const uint32_t old = GB[nc];
+        oldg = (old & 0x80u) ? man + 2u * (old & 31u) : 0xFFFFFFFFu;
+      } else {
+        const uint32_t old = GS[nc];
+        oldg = ((old & 0xFFC00000u) == tagw) ? (old & GS_G_MASK) : 0xFFFFFFFFu;
+      }
+      if (tg < oldg) {
+        const uint32_t lab = cg == 0 ? d : labc;
+        const uint32_t h = (nx > gx ? nx - gx : gx - nx) + (ny > gy ? ny - gy : gy - ny);
+        const uint32_t f = tg + h;
+        bool ovf = len >= hcap || tg >= (1u << 15) || f >= (1u << 17);
+        if constexpr (GSM == 2) {
+          const uint32_t hh = (tg - man) >> 1;
+          ovf = ovf || hh > 31u;
+          if (!ovf) GB[nc] = (uint8_t)(0x80u | (lab << 5) | hh);
+        } else {
+          if (!ovf) GS[nc] = tagw | (lab << 20) | tg;
+        }
+        if (ovf) {
+          *len_out = -2;
+          return NH_UNKNOWN;
+        }
+        hk_sift_up(Hp, len, ((uint64_t)((f << 15) | tg) << 32) | (nx << 16) | ny);
+        ++len;
+      }
+    }
+  }
+  *len_out = 2;
+  return fallback_code(G.nbmask[v], vx, vy, gx, gy);
+}
+
+// ----------------------------------------------------------------------------
+// Wave-cooperative A* core (k_astar_wave default; TSW_ASTAR_SERIAL=1 selects the lone-lane
+// core above). Same BinaryHeap algorithm, same heap contents after every operation — only the
+// way each sift touches its path changes, so the pop order (and every label) is identical:
+//  * sift_down_to_bottom: the 62 descendants of the hole within 5 levels are read by one
+//    ds_read (lane j -> depth k = log2(j + 2), index j + 2 - 2^k below the hole). Each left
+//    child compares its key with its sibling's (DPP lane swap); "take the right child" bits and
+//    the node-exists bits are balloted, and the path (left <= right -> right child, a lone left
+//    child is taken, stop at a childless node) is walked in SALU. The path's values move up one
+//    level with one ds_write. A 4096-entry heap has depth 12: <= 3 LDS round trips per pop
+//    instead of 12 dependent ones.
+//  * sift_up (of the popped-last element and of every push): the hole's ancestors are read one
+//    per lane. The root path is heap ordered, so the ancestors whose key exceeds the element's
+//    (those the element passes: it stops at the first parent it is not smaller than) are a
+//    suffix of it: one ballot gives the landing depth and one ds_write shifts them down.
+//  * the four neighbours are relaxed by lanes 0..3 at once (distinct cells); the improved
+//    ones are pushed in direction order (tswap.rs:337-360's loop order).
+// LDS instructions of one wave complete in issue order, so a lane reads what another lane of
+// the same wave wrote by an earlier instruction.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rl32(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t l) {
+  return ((uint64_t)rl32((uint32_t)(x >> 32), l) << 32) | rl32((uint32_t)x, l);
+}
+__device__ __forceinline__ void wave_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ uint64_t ballot64(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
+// BinaryHeap::sift_up(0, pos) with `elem` in the hole; wave-uniform arguments. Straight-line:
+// every lane reads (lanes >= the hole's depth re-read the hole), one ballot, one store.
+__device__ __forceinline__ void wsift_up(uint64_t* Hp, uint32_t pos, uint64_t elem, uint32_t lane) {
+  const uint32_t p1 = pos + 1u;
+  const uint32_t dp = 31u - (uint32_t)__builtin_clz(p1);  // depth of the hole (root = 0)
+  const uint32_t k = hk(elem);
+  const uint32_t sh = dp > lane ? dp - lane : 0u;
+  const uint64_t a = Hp[(p1 >> sh) - 1u];  // ancestor at depth `lane`
+  const uint64_t G = ballot64(k < hk(a)) & ((1ull << dp) - 1ull);  // ancestors elem moves past
+  const uint32_t t = dp - (uint32_t)__popcll(G);                   // landing depth
+  const bool isdp = lane == dp;
+  // lanes t..dp-1 move their ancestor one level down the path; lane dp stores elem at depth t
+  const uint32_t dst = isdp ? (p1 >> (dp - t)) - 1u : (p1 >> (sh - 1u)) - 1u;
+  wave_order();
+  if (lane >= t && lane <= dp) Hp[dst] = isdp ? elem : a;
+  wave_order();
+}
+
+// BinaryHeap::pop (swap last into the root, sift_down_to_bottom(0), sift_up(0, hole)); len >= 1.
+// Window lanes: lane j < 62 <-> depth kk = log2(j + 2) (1..5), index ki = j + 2 - 2^kk below the
+// hole; the first window's lanes 62 / 63 fetch the last element / the root.
+__device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t lane) {
+  constexpr uint64_t M62 = (1ull << 62) - 1ull, EVEN = 0x5555555555555555ull;
+  const uint32_t end = --len;
+  uint32_t pos = 0;
+  uint64_t last = 0, top = 0;
+  const uint32_t kk = 31u - (uint32_t)__builtin_clz(lane + 2u);
+  const uint32_t ki = lane + 2u - (1u << kk);
+  for (bool first = true;; first = false) {
+    const uint32_t node = ((pos + 1u) << kk) - 1u + ki;
+    uint32_t addr = node < end ? node : end;  // Hp[end] is still allocated
+    if (first) addr = lane == 62u ? end : (lane == 63u ? 0u : addr);
+    const uint64_t val = Hp[addr];
+    if (first) {
+      last = rl64(val, 62);
+      top = rl64(val, 63);
+      if (end == 0) return last;
+    }
+    const uint32_t key = hk(val);
+    const uint32_t sib = (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    const uint64_t VL = ballot64(node < end) & M62;
+    // left child lane (even) takes the right child when left <= right and the right exists
+    const uint64_t CR = ballot64(key >= sib) & (VL >> 1) & EVEN;
+    uint32_t idx = 0, d = 0, live = 1;
+#pragma unroll
+    for (uint32_t k = 1; k <= 5; ++k) {  // branch-free SALU walk down the path
+      const uint32_t ll = (1u << k) - 2u + 2u * idx;
+      live &= (uint32_t)(VL >> ll) & 1u;
+      idx = live ? 2u * idx + ((uint32_t)(CR >> ll) & 1u) : idx;
+      d += live;
+    }
+    if (d == 0) break;
+    const bool on = kk <= d && ki == (idx >> (d - kk));
+    wave_order();
+    if (on) Hp[(node - 1u) >> 1] = val;  // move up into the parent
+    wave_order();
+    pos = ((pos + 1u) << d) - 1u + idx;
+    if (d < 5) break;
+  }
+  wsift_up(Hp, pos, last, lane);
+  return top;
+}
+
+// FB: the grid's free-cell row bitmap (DevGrid::freebits) staged in LDS, so relaxing a node
+// needs no global load.
+// PROF: pr[0..4] = pops, clocks in pops, in relaxations, in pushes, pushes (TSW_ASTAR_PROF)
+template <int GSM, bool PROF>
+__device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag,
+                                                  uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
+                                                  const uint32_t* FB, int32_t* len_out, unsigned long long* pr) {
+  const uint32_t lane = threadIdx.x & 63u;
+  unsigned long long pops = 0, c_pop = 0, c_nb = 0, c_push = 0, npush = 0, tk = 0;
+  auto tick = [&](unsigned long long& acc) {
+    if constexpr (PROF) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc += t - tk;
+      tk = t;
+    }
+  };
+  auto flush = [&]() {
+    if constexpr (PROF) {
+      pr[0] = pops;
+      pr[1] = c_pop;
+      pr[2] = c_nb;
+      pr[3] = c_push;
+      pr[4] = npush;
+    }
+  };
+  const uint32_t W = G.W, H = G.H, Ww = G.Ww;
+  const uint32_t vy = v / W, vx = v - vy * W, gy = goal / W, gx = goal - gy * W;
+  if (v == goal) {
+    *len_out = 1;
+    return NH_STAY;
+  }
+  const uint32_t tagw = tag << 22;
+  const uint32_t h0 = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
+  if (h0 >= (1u << 17)) {
+    *len_out = -2;
+    return NH_UNKNOWN;
+  }
+  if (lane == 0) {
+    if constexpr (GSM == 2) GB[v] = 0x80u;
+    else GS[v] = tagw;
+    Hp[0] = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
+  }
+  wave_order();
+  if constexpr (PROF) tk = __builtin_amdgcn_s_memtime();
+  uint32_t len = 1;
+  // lanes 0..3 own the neighbour in direction `lane` (S, E, N, W: tswap.rs:62-73)
+  const uint32_t dd = lane & 3u;
+  while (len > 0) {
+    ++pops;
+    const uint64_t e = wpop(Hp, len, lane);
+    tick(c_pop);
+    const uint32_t cx = (uint32_t)(e >> 16) & 0xFFFFu, cy = (uint32_t)e & 0xFFFFu;
+    const uint32_t cg = hk(e) & 0x7FFFu;
+    const uint32_t c = cy * W + cx;
+    if (c == goal) {
+      flush();
+      *len_out = (int32_t)cg + 1;
+      if constexpr (GSM == 2) return (uint8_t)((GB[goal] >> 5) & 3u);
+      else return (uint8_t)((GS[goal] >> 20) & 3u);
+    }
+    // neighbour of lane dd (unsigned wrap: x - 1 at x = 0 fails the bound test); every lane
+    // reads (out-of-grid lanes re-read the popped cell), the LDS reads issue together
+    const uint32_t nx = dd == 1 ? cx + 1 : (dd == 3 ? cx - 1 : cx);
+    const uint32_t ny = dd == 0 ? cy + 1 : (dd == 2 ? cy - 1 : cy);
+    const bool inb = lane < 4u && nx < W && ny < H;
+    const uint32_t fx = inb ? nx : cx, fy = inb ? ny : cy;
+    const uint32_t nc = fy * W + fx;
+    const uint32_t fw = FB[fy * Ww + (fx >> 5)];
+    uint32_t old, labc;
+    if constexpr (GSM == 2) {
+      old = GB[nc];
+      labc = (GB[c] >> 5) & 3u;
+    } else {
+      old = GS[nc];
+      labc = (GS[c] >> 20) & 3u;
+    }
+    const uint32_t tg = cg + 1u;
+    uint32_t oldg, man = 0;
+    if constexpr (GSM == 2) {
+      man = (fx > vx ? fx - vx : vx - fx) + (fy > vy ? fy - vy : vy - fy);
+      oldg = (old & 0x80u) ? man + 2u * (old & 31u) : 0xFFFFFFFFu;
+    } else {
+      oldg = ((old & 0xFFC00000u) == tagw) ? (old & GS_G_MASK) : 0xFFFFFFFFu;
+    }
+    const bool imp = inb && ((fw >> (fx & 31u)) & 1u) && tg < oldg;
+    uint64_t ent = 0;
+    bool ovf = false;
+    if (imp) {
+      const uint32_t lab = cg == 0 ? dd : labc;
+      const uint32_t h = (fx > gx ? fx - gx : gx - fx) + (fy > gy ? fy - gy : gy - fy);
+      const uint32_t f = tg + h;
+      ovf = tg >= (1u << 15) || f >= (1u << 17);
+      if constexpr (GSM == 2) {
+        const uint32_t hh = (tg - man) >> 1;
+        ovf = ovf || hh > 31u;
+        if (!ovf) GB[nc] = (uint8_t)(0x80u | (lab << 5) | hh);
+      } else {
+        if (!ovf) GS[nc] = tagw | (lab << 20) | tg;
+      }
+      ent = ((uint64_t)((f << 15) | tg) << 32) | (fx << 16) | fy;
+    }
+    uint64_t M = ballot64(imp);
+    tick(c_nb);
+    if (ballot64(ovf) != 0ull || len + (uint32_t)__popcll(M) > hcap) {
+      *len_out = -2;
+      return NH_UNKNOWN;
+    }
+    wave_order();
+    while (M) {
+      const uint32_t d = (uint32_t)__builtin_ctzll(M);
+      M &= M - 1ull;
+      wsift_up(Hp, len, rl64(ent, d), lane);
+      ++len;
+      ++npush;
+    }
+    tick(c_push);
+  }
+  flush();
+  *len_out = 2;
+  return fallback_code(G.nbmask[v], vx, vy, gx, gy);
+}
+
+}  // namespace tsw

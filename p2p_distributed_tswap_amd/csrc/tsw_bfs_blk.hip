@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       const uint32_t bx = p - __umulhi(p, A.bp_magic) * Bp;
       const uint64_t wf = ((f0 << 1) & ~COL0) | ((bx & 3u) ? ((fw >> 7) & COL0) : 0ull);
       const uint64_t rs = f0 & ~wf;
-      uint64_t rsn = (A.dbg & 4u) ? 0ull : nw & rs;
+      uint64_t rsn = (TSW_DIAG_BITS(A.dbg) & 4u) ? 0ull : nw & rs;
       while (rsn) {
         const uint32_t bb = (uint32_t)__builtin_ctzll(rsn);
         anch[AB[p] + (uint32_t)__popcll(rs & ((1ull << bb) - 1ull))] = (uint16_t)lvl;
@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
       const uint32_t wf = ((f0 << 1) & ~C0) | ((bx & 3u) ? ((fw >> 7) & C0) : 0u);
       const uint32_t rs = f0 & ~wf;
       const uint32_t below = __popc(partner(rs));  // the low half's run starts precede ours
-      uint32_t rsn = (A.dbg & 4u) ? 0u : nw & rs;
+      uint32_t rsn = (TSW_DIAG_BITS(A.dbg) & 4u) ? 0u : nw & rs;
       const uint32_t base = abp + (h ? below : 0u);
       while (rsn) {
         const uint32_t bb = (uint32_t)__builtin_ctz(rsn);
@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         // zero guard block
         V[p] = vv;
         const uint64_t wln = nw & (((v0 << 1) & ~COL0) | ((vw >> 7) & COL0));
-        if (wln && !(A.dbg & 2u)) {
+        if (wln && !(TSW_DIAG_BITS(A.dbg) & 2u)) {
           if constexpr (WLS) WL[p] |= wln;  // owner-exclusive within the level, program order across levels
           else wl_or(WL + p, (unsigned long long)wln);
         }
@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
         const uint32_t vv = v0 | nw;
         V32[o] = vv;  // owner-exclusive (deduplicated list, one lane per half); idle lanes rewrite 0
         const uint32_t wln = nw & (((v0 << 1) & ~C0) | ((vw >> 7) & C0));
-        if (wln && !(A.dbg & 2u)) {
+        if (wln && !(TSW_DIAG_BITS(A.dbg) & 2u)) {
           if constexpr (WLS) WL32[o] |= wln;
           else wl_or32(WL32 + o, wln);
         }
@@ -618,7 +618,7 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
           const uint32_t c0 = base + 8u * q;
           if (c0 >= cs && c0 + 8u <= ce) {
             const uint4 v4 = *reinterpret_cast<const uint4*>(LS + 8u * q);
-            if (A.dbg & 1u) {
+            if (TSW_DIAG_BITS(A.dbg) & 1u) {
               typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
               const u32x4 vv = {v4.x, v4.y, v4.z, v4.w};
               __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(D + c0));

@@ -44,9 +44,11 @@ struct DevStatus {
 
 enum { CAT_BFS = 0, CAT_ASTAR = 1, CAT_WALK = 2, CAT_ASSIGN = 3, NCAT = 4 };
 
-// Diagnostic / A-B knobs. Read ONCE from the environment when the context is created (never on a
-// call path), so a context's behaviour cannot change under it. None changes a result: every
-// setting is covered by a bit-exact test. Defaults are the production configuration.
+// Diagnostic / A-B knobs. The production library (libtswap_hip.so) never reads the environment:
+// these are its fixed defaults, and the only caller-visible options are tsw_opts (include/tswap.h).
+// The diagnostic build (libtswap_hip_diag.so, -DTSW_DIAG, __graft_entry__.build) reads the TSW_*
+// variables below ONCE when a context is created — kernel A/B variants, instrumentation, and
+// TSW_BFS_DBG, which drops work and writes WRONG tables (measurement only).
 struct Tunables {
   uint32_t bfs_mode = 0;          // TSW_BFS_KERNEL: 0 auto, 1 wave (row words), 2 block, 3 blk (8x8), 4 big
   uint32_t bfs_cap = 512;         // TSW_BFS_LISTCAP: k_bfs_wave LDS list entries
@@ -79,6 +81,7 @@ struct Tunables {
 
   static Tunables from_env() {
     Tunables t;
+#ifdef TSW_DIAG
     auto num = [](const char* k, long lo, long hi, long def) -> long {
       const char* v = getenv(k);
       if (!v) return def;
@@ -113,6 +116,7 @@ struct Tunables {
     t.chain_preempt = num("TSW_CHAIN_PREEMPT", 0, 1, 1) != 0;
     t.avoid_xcc = num("TSW_WORKER_AVOID_XCD", 0, 1, 1) != 0;
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
+#endif
     return t;
   }
 };
@@ -181,8 +185,7 @@ struct tsw_ctx {
   int32_t* d_lens = nullptr;
   size_t rescap = 0;
 
-  // coop mode: K3 workers concurrent with the planner (second stream, control block, queues)
-  hipStream_t s2 = nullptr;
+  // coop mode: K3 workers in the plan dispatch beside the planner (control block, queues)
   CoopCtl* d_cc = nullptr;
   CoopCtl* h_cc = nullptr;       // pinned
   AstarQuery* d_QS = nullptr;
@@ -193,6 +196,7 @@ struct tsw_ctx {
   uint32_t* h_flags = nullptr;   // pinned, coherent: [0] planner resident, [1] abort, [2] heartbeat
   uint32_t* d_flags = nullptr;
   uint64_t coop_aborts = 0;
+  uint32_t watchdog_ms = 10000;  // tsw_opts.watchdog_ms
 
   DevStatus* d_stat = nullptr;
   DevStatus* h_stat = nullptr;   // pinned, D2H
@@ -625,7 +629,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
       nbw = std::min(max_waves, bfs_blk_waves_per_block(c->nbp, c->tun.blk_cap, c->max_lds, c->tun.bfs_wls != 0u, false));
     }
   }
-  if (nbw == 0 && bfs_mode == 3) RET(TSW_EINVAL, "k_bfs_blk does not fit this grid (TSW_BFS_KERNEL=blk)");
+  if (nbw == 0 && bfs_mode == 3) RET(TSW_EINVAL, "k_bfs_blk does not fit this grid (forced kernel blk)");
   if (nbw > 0) {
     Timer t(c, CAT_BFS);
     // scratch per goal slot: one per wave, two with TSW_BFS_PAIR
@@ -677,7 +681,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   uint32_t nwv = 0;
   if ((bfs_mode == 0 || bfs_mode == 1) && c->npw <= 0x8000u)
     nwv = bfs_wave_waves_per_block(c->npw, c->tun.bfs_cap, c->max_lds);
-  if (nwv == 0 && bfs_mode == 1) RET(TSW_EINVAL, "k_bfs_wave does not fit this grid (TSW_BFS_KERNEL=wave)");
+  if (nwv == 0 && bfs_mode == 1) RET(TSW_EINVAL, "k_bfs_wave does not fit this grid (forced kernel wave)");
   uint32_t big_cap = 0;
   if (nwv == 0 && (bfs_mode == 0 || bfs_mode == 4) && bfs_big_fits(c->nbp, c->max_lds, &big_cap)) {
     // large grids (e.g. 1024x1024): one workgroup per goal, shared visited bitmap in LDS
@@ -720,7 +724,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     if (nh) HIPCHK(launch_classify(c->G, goals, slots, k, dist, dstride, nh, c->s));
     return TSW_OK;
   }
-  if (bfs_mode == 4) RET(TSW_EINVAL, "k_bfs_big does not fit this grid (TSW_BFS_KERNEL=big)");
+  if (bfs_mode == 4) RET(TSW_EINVAL, "k_bfs_big does not fit this grid (forced kernel big)");
   Timer t(c, CAT_BFS);
   if (nwv == 0) {
     HIPCHK(launch_bfs(c->G, goals, slots, k, dist, dstride, nh, dstride, &c->d_stat->err, c->max_lds, c->num_cu,
@@ -945,7 +949,6 @@ int ensure_coop(tsw_ctx* c, uint32_t n) {
   if (!c->d_cc) {
     HIPCHK(hipMalloc(&c->d_cc, sizeof(CoopCtl)));
     HIPCHK(hipHostMalloc(&c->h_cc, sizeof(CoopCtl), hipHostMallocDefault));
-    HIPCHK(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
   }
   if (!c->d_QS) {
     HIPCHK(hipStreamSynchronize(c->s));
@@ -1050,10 +1053,9 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   // one lane per agent in the parallel passes when possible; >= 4 waves for the task argmin
   uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
   if (c->tun.plan_block) block = std::max<uint32_t>(64u, c->tun.plan_block);
-  const bool coop = P.coop != 0;
   WorkerArgs W{};
-  WorkerCfg wcfg{};
-  if (coop) {
+  uint32_t wblocks = 0;
+  if (P.coop) {
     W.G = c->G;
     W.cc = c->d_cc;
     W.QN = c->d_Q;
@@ -1061,7 +1063,6 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.QT = c->d_QT;
     W.nh = c->d_nh;
     W.nstride = c->tstride;
-    W.hcap = c->tun.wave_hcap;
     // task chains take half the workers at most (a quarter with many agents: their needed bursts
     // are larger), the rest stay free for the pairs the planner waits on
     W.tmask = P.n > 2000u ? 3u : 1u;
@@ -1072,12 +1073,25 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.epochs = c->d_epochs;
     W.heaps = c->d_heaps;
     W.ghcap = c->hcap;
-    wcfg = worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs);
+    const WorkerCfg wcfg = worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs);
+    W.gs_lds = wcfg.gs_lds;
+    W.stage_fb = wcfg.stage_fb;
+    W.hcap = wcfg.hcap;
+    // one dispatch: the planner (workgroup 0) and one worker workgroup on every other CU, each holding
+    // as many single-wave workers as its dynamic LDS (the planner's, whole-CU size) carves
+    W.lds_per_wave = (uint32_t)((wcfg.lds + 15u) & ~(size_t)15u);
+    W.wpb = W.lds_per_wave ? (uint32_t)std::min<size_t>(block / 64u, lds / W.lds_per_wave) : 0u;
+    const uint32_t want = W.wpb * (uint32_t)std::max(c->num_cu - 1, 0);
+    W.nworkers = std::min(want, c->nslots);
+    wblocks = W.wpb ? (W.nworkers + W.wpb - 1u) / W.wpb : 0u;
     if (c->tun.plan_debug)
-      fprintf(stderr, "[k_plan] workers: %u waves, g-scores %u, heap %u entries, %zu B LDS\n", wcfg.waves, wcfg.gs_lds,
-              wcfg.hcap, wcfg.lds);
-    wcfg.waves = std::min(wcfg.waves, c->nslots);
+      fprintf(stderr, "[k_plan] workers: %u waves (%u per workgroup), g-scores %u, heap %u entries, %u B LDS each\n",
+              W.nworkers, W.wpb, wcfg.gs_lds, wcfg.hcap, W.lds_per_wave);
+    if (W.nworkers == 0 || wcfg.hcap < 4u) P.coop = 0;  // nothing fits beside the planner: exit mode
   }
+  const bool coop = P.coop != 0;
+  // every return below happens after the dispatch has drained (workers included): nothing of this
+  // call keeps running into the next one
   for (uint64_t round = 0;; ++round) {
     if (round > 16ull * P.n + 4096ull * (init.max_t + 1)) RET(TSW_EINVAL, "plan kernel made no progress");
     if (coop) {
@@ -1093,20 +1107,11 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     }
     {
       Timer t(c, CAT_WALK);
-      HIPCHK(launch_plan(P, lds, block, c->s));
+      HIPCHK(launch_plan(P, coop ? &W : nullptr, wblocks, lds, block, c->s));
       c->st.plan_block = block;
     }
     c->st.walker_launches++;
-    if (coop) {
-      // the workers go on the second stream once the planner block is resident (it sets the flag
-      // first thing), so they can never take the CU it needs; if the flag is late they start anyway
-      // and the planner falls back to exits (no deadlock either way)
-      const auto t0 = std::chrono::steady_clock::now();
-      while (!c->h_flags[0] && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(500)) {
-      }
-      HIPCHK(launch_astar_workers(W, wcfg, c->s2));
-      c->st.astar_launches++;
-    }
+    if (coop) c->st.astar_launches++;
     HIPCHK(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(PlanCtl), hipMemcpyDeviceToHost, c->s));
     {
       // watchdog: the planner publishes its timestep count; if it stops moving for 10 s while the
@@ -1126,17 +1131,19 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
         if (hb != last) {
           last = hb;
           seen = now;
-        } else if (!hf[1] && now - seen > std::chrono::seconds(10)) {
+        } else if (!hf[1] && now - seen > std::chrono::milliseconds(c->watchdog_ms)) {
           hf[1] = 1u;
           ++c->coop_aborts;
-          fprintf(stderr, "[tswap] coop watchdog: planner made no step for 10 s; falling back to exit mode\n");
+          ++c->st.watchdog_fires;
+          if (c->watchdog_ms >= 1000u)
+            fprintf(stderr, "[tswap] watchdog: planner made no step for %u ms; finishing the call in exit mode\n",
+                    c->watchdog_ms);
         }
         std::this_thread::sleep_for(std::chrono::microseconds(50));
       }
     }
     HIPCHK(hipStreamSynchronize(c->s));
     if (coop) {
-      HIPCHK(hipStreamSynchronize(c->s2));
       HIPCHK(hipMemcpy(c->h_cc, c->d_cc, sizeof(CoopCtl), hipMemcpyDeviceToHost));
       const CoopCtl& cc = *c->h_cc;
       c->st.coop_waits += cc.waits;
@@ -1146,6 +1153,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
         c->st.coop_waits_sec[k] += cc.waits_sec[k];
       }
       c->st.astar_queries += cc.worker_queries;
+      c->st.coop_workers = W.nworkers;
+      for (int k = 0; k < 3; ++k) c->st.coop_worker_busy_ms[k] += (double)cc.wbusy[k] / (double)c->wall_khz;
       if (cc.err) RET(TSW_EOVERFLOW, "K3 worker: A* heap overflow");
       // speculative pairs nobody claimed stay PENDING_S: back to UNKNOWN for later calls
       if (cc.head_s > cc.claim_s) {
@@ -1157,8 +1166,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     if (k.err & ERR_ABORT) {
       char buf[256];
       snprintf(buf, sizeof buf,
-               "planner stopped by the watchdog (no timestep for 10 s): t %u section %u cursor %u, %u rule rounds, "
-               "%u move rounds", k.t, k.section, k.i, k.rule_rounds, k.move_rounds);
+               "planner stopped by the watchdog (no timestep for %u ms): t %u section %u cursor %u, %u rule rounds, "
+               "%u move rounds", c->watchdog_ms, k.t, k.section, k.i, k.rule_rounds, k.move_rounds);
       RET(TSW_EINVAL, buf);
     }
     if (k.err) {
@@ -1371,9 +1380,11 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
     return nullptr;
   }
   tsw_ctx* c = new tsw_ctx();
-  c->tun = Tunables::from_env();  // the only place the environment is read
+  c->tun = Tunables::from_env();  // diagnostic build only: the only place the environment is read
   c->device = opts ? opts->device : 0;
   c->flags = opts ? opts->flags : 0;
+  if (c->flags & TSW_F_EXIT_MODE) c->tun.coop = false;
+  if (opts && opts->watchdog_ms) c->watchdog_ms = opts->watchdog_ms;
   if (c->device < 0 || c->device >= ndev) {
     g_create_err = "tsw_create: bad device ordinal";
     delete c;
@@ -1512,7 +1523,6 @@ void tsw_destroy(tsw_ctx* c) {
   fre(c->d_cc); fre(c->d_QS); fre(c->d_QT);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
-  if (c->s2) (void)hipStreamDestroy(c->s2);
   if (c->h_stat) hipHostFree(c->h_stat);
   if (c->h_ctl) hipHostFree(c->h_ctl);
   for (auto& e : c->pending) {

@@ -18,6 +18,14 @@
 #pragma once
 #include <stdint.h>
 
+// Diagnostic-build switches (-DTSW_DIAG, libtswap_hip_diag.so): in the production build every
+// diagnostic bit reads as 0, so the code paths that drop work for measurement are compiled out.
+#ifdef TSW_DIAG
+#define TSW_DIAG_BITS(x) (x)
+#else
+#define TSW_DIAG_BITS(x) 0u
+#endif
+
 namespace tsw {
 
 constexpr uint8_t NH_STAY = 4;

@@ -99,11 +99,10 @@ size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool 
                       bool mu = true);
 hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, uint32_t* dups,
                       hipStream_t s);
-hipError_t launch_plan(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s);
-
-// Persistent K3 worker waves for coop mode (tsw_kernels.hip): claim queued pairs from cc's queues
-// (needed first), resolve them with the exact A* and write the next-hop code; exit when the planner
-// has stopped and the needed queue is drained (speculative leftovers are abandoned).
+// Coop-mode K3 workers (tsw_worker.h) run in the workgroups 1.. of the plan dispatch: claim queued
+// pairs from cc's queues (needed first), resolve them with the exact A* and write the next-hop code;
+// exit when the planner has stopped and the needed queue is drained (speculative leftovers are
+// abandoned).
 struct WorkerArgs {
   DevGrid G;
   CoopCtl* cc;
@@ -123,6 +122,9 @@ struct WorkerArgs {
   uint64_t* heaps;    // per-wave global heaps (tier 3), ghcap entries each
   uint32_t ghcap;
   uint32_t avoid_xcc;  // workers placed on the planner's XCD exit at once (its L2 stays the planner's)
+  uint32_t wpb;        // worker waves per workgroup (each owns lds_per_wave bytes of the dynamic LDS)
+  uint32_t lds_per_wave;
+  uint32_t nworkers;   // worker waves in the dispatch (<= the global g-score / heap slots)
 };
 // Worker placement: per-wave LDS (heap, g-scores, free bitmap) sets the waves per CU. g-scores stay
 // in LDS (fastest per pop) unless that leaves < 3 waves per CU while many agents can need queries at
@@ -132,6 +134,10 @@ struct WorkerCfg {
   size_t lds;
 };
 WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs = -1);
-hipError_t launch_astar_workers(const WorkerArgs& A, const WorkerCfg& cfg, hipStream_t s);
+
+// The plan dispatch: workgroup 0 runs k_plan's planner (block threads, lds bytes of dynamic LDS);
+// with W (coop mode) workgroups 1..worker_blocks run W->wpb K3 worker waves each.
+hipError_t launch_plan(const PlanArgs& P, const WorkerArgs* W, uint32_t worker_blocks, size_t lds, uint32_t block,
+                       hipStream_t s);
 
 }  // namespace tsw

@@ -29,8 +29,10 @@
 // and relaunches.
 #include <hip/hip_runtime.h>
 
+#include "tsw_astar.h"
 #include "tsw_internal.h"
 #include "tsw_plan.h"
+#include "tsw_worker.h"
 
 namespace tsw {
 
@@ -46,16 +48,6 @@ constexpr uint32_t NO_CELL = 0xFFFFFFFFu;
 constexpr uint32_t LIST_CAP = 1024;  // entries of the kernel's LDS `list` (ASSIGN compaction, changed agents)
 // movement-round decision states
 constexpr uint8_t DEC_OPEN = 0, DEC_DONE = 1, DEC_STAY = 2, DEC_MOVE = 3, DEC_SWAP = 4;
-
-__device__ __forceinline__ uint32_t step_cell(uint32_t c, uint32_t code, uint32_t W) {
-  switch (code) {
-    case 0: return c + W;
-    case 1: return c + 1;
-    case 2: return c - W;
-    case 3: return c - 1;
-    default: return c;
-  }
-}
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
 #pragma unroll
@@ -98,6 +90,7 @@ struct Arrays {
   uint64_t* MU;    // per cell: (round << 32) | ~(lowest undecided agent targeting it), movement rounds
   const uint32_t* PXY;
   uint8_t* USED;
+  unsigned long long t0;  // wall clock at the launch (coop: "no worker has started" is measured from here)
 };
 
 // Next-hop code of (v, goal slot tab). A plain load may return a stale PENDING from this XCD's L2
@@ -401,7 +394,7 @@ __device__ __forceinline__ void coop_publish(const PlanArgs& P, uint32_t* s_q) {
   __hip_atomic_store(&P.cc->pub, s_q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr unsigned long long COOP_NO_WORKER_TICKS = 5000000ull;  // 50 ms at 100 MHz: workers never started
+constexpr unsigned long long COOP_NO_WORKER_TICKS = 100000ull;    // 1 ms at 100 MHz after the launch: no worker running
 constexpr unsigned long long COOP_RETRY_TICKS = 2000000ull;      // 20 ms pending: queue the pair again
 constexpr unsigned long long COOP_GIVE_UP_TICKS = 500000000ull;  // 5 s: safety valve
 enum : int { COOP_OK = 0, COOP_GIVE_UP = 1, COOP_RETRY = 2 };
@@ -444,7 +437,7 @@ __device__ int coop_wait(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint
       if (c == NH_UNKNOWN) break;
       const unsigned long long dt = wall_clock64() - t0;
       if (dt > COOP_GIVE_UP_TICKS || ld_agent(&P.cc->err) != 0u ||
-          (dt > COOP_NO_WORKER_TICKS && ld_agent(&P.cc->alive) == 0u) ||
+          (ld_agent(&P.cc->alive) == 0u && wall_clock64() - S.t0 > COOP_NO_WORKER_TICKS) ||
           (P.hflags && __hip_atomic_load(&P.hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
         st = COOP_GIVE_UP;
         break;
@@ -742,8 +735,16 @@ __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
 // AG: every agent array in LDS. OC: the occupancy grid OCC in LDS; MUL: the movement rounds' MU
 // words too (OC alone fits grids whose MU does not, e.g. C3's 170x84 beside the agent arrays).
 template <bool AG, bool OC, bool MUL>
-__global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
+__global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
   extern __shared__ __align__(16) uint8_t smem[];
+  if (blockIdx.x != 0) {  // coop mode: a K3 worker workgroup (tsw_worker.h), Wk.wpb single-wave workers
+    const uint32_t w = threadIdx.x >> 6;
+    if (w < Wk.wpb) {
+      const uint32_t wid = (blockIdx.x - 1u) * Wk.wpb + w;
+      if (wid < Wk.nworkers) coop_worker(Wk, reinterpret_cast<uint64_t*>(smem + (size_t)w * Wk.lds_per_wave), wid);
+    }
+    return;
+  }
   __shared__ PlanCtl s_ctl;
   __shared__ uint32_t s_q[5], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
   __shared__ uint32_t s_wcount[16];
@@ -755,7 +756,12 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
   const uint32_t n = P.n, W = P.W;
 
   // ---- carve LDS (order must match plan_lds_bytes) ---------------------------
+  // coop mode: the XCD this block runs on, first thing — workers placed on it leave (their g-score
+  // traffic would share the planner's L2; TSW_WORKER_AVOID_XCD)
+  if (P.coop && threadIdx.x == 0)
+    __hip_atomic_store(&P.cc->planner_xcc, 1u + hw_xcc_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   Arrays S;
+  S.t0 = wall_clock64();
   uint8_t* p = smem;
   auto carve = [&](size_t bytes) {
     uint8_t* r = p;
@@ -841,13 +847,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P) {
     for (int k = 0; k < 32; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
-    // coop mode: tell the host the planner is resident, so the workers it launches next cannot
-    // take the CUs this block needs
+    // the host's watchdog: the planner block is resident
     if (P.hflags) {
-      // the XCD this block runs on: workers the host launches next skip it (TSW_WORKER_AVOID_XCD)
-      if (P.coop)
-        __hip_atomic_store(&P.cc->planner_xcc, 1u + (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&P.hflags[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
@@ -1911,22 +1912,28 @@ hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cn
 }
 
 template <bool AG, bool OC, bool MUL>
-static hipError_t launch_plan_t(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s) {
+static hipError_t launch_plan_t(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+                                hipStream_t s) {
   hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC, MUL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_plan<AG, OC, MUL>), dim3(1), dim3(block), lds, s, P);
+  hipLaunchKernelGGL((k_plan<AG, OC, MUL>), dim3(grid), dim3(block), lds, s, P, W);
   return hipGetLastError();
 }
 
-hipError_t launch_plan(const PlanArgs& P, size_t lds, uint32_t block, hipStream_t s) {
+hipError_t launch_plan(const PlanArgs& P, const WorkerArgs* W, uint32_t worker_blocks, size_t lds, uint32_t block,
+                       hipStream_t s) {
+  WorkerArgs none{};
+  const WorkerArgs& A = (W && P.coop) ? *W : none;
+  const uint32_t grid = 1u + ((W && P.coop) ? worker_blocks : 0u);
+  if (grid > 1u && ((size_t)A.wpb * A.lds_per_wave > lds || A.wpb * 64u > block)) return hipErrorInvalidValue;
   const bool mu = P.occ_lds && P.mu_lds;
-  if (P.agents_lds && mu) return launch_plan_t<true, true, true>(P, lds, block, s);
-  if (P.agents_lds && P.occ_lds) return launch_plan_t<true, true, false>(P, lds, block, s);
-  if (P.agents_lds) return launch_plan_t<true, false, false>(P, lds, block, s);
-  if (mu) return launch_plan_t<false, true, true>(P, lds, block, s);
-  if (P.occ_lds) return launch_plan_t<false, true, false>(P, lds, block, s);
-  return launch_plan_t<false, false, false>(P, lds, block, s);
+  if (P.agents_lds && mu) return launch_plan_t<true, true, true>(P, A, grid, lds, block, s);
+  if (P.agents_lds && P.occ_lds) return launch_plan_t<true, true, false>(P, A, grid, lds, block, s);
+  if (P.agents_lds) return launch_plan_t<true, false, false>(P, A, grid, lds, block, s);
+  if (mu) return launch_plan_t<false, true, true>(P, A, grid, lds, block, s);
+  if (P.occ_lds) return launch_plan_t<false, true, false>(P, A, grid, lds, block, s);
+  return launch_plan_t<false, false, false>(P, A, grid, lds, block, s);
 }
 
 }  // namespace tsw

@@ -1,0 +1,301 @@
+// tsw_worker.h — coop-mode K3 workers: the exact A* (tsw_astar.h) run by the non-planner
+// workgroups of the plan dispatch (k_plan, tsw_plan.hip) CONCURRENTLY with the planner block.
+//
+// One dispatch holds the planner (workgroup 0) and one worker workgroup per other CU; a worker
+// workgroup runs `wpb` independent single-wave workers (the rest of its waves leave at once), each
+// with its own slice of the workgroup's LDS (heap, g-scores, free-cell bitmap). Being one dispatch,
+// the planner and its workers are resident together whatever serialises dispatches (a profiler's
+// counter passes, another queue): nothing waits on a kernel that has not started. Workers never
+// execute s_barrier (their waves run unrelated queries); LDS ordering within a wave is
+// wave_order() — LDS instructions of one wave complete in issue order.
+//
+// Protocol (CoopCtl, tsw_internal.h): the planner appends (cell, goal) pairs to two queues —
+// needed pairs (a step is waiting on them) and speculative prefetches — and publishes the heads;
+// each worker claims one pair at a time (needed first, CAS on the claim counter), runs the A*
+// (same BinaryHeap order and hand-off chain as k_astar_wave: LDS heap + LDS g-scores -> LDS heap +
+// global u32 g-scores -> global heap) and stores the code into the next-hop table with an
+// agent-scope store the planner polls. Task chains (every task's pickup -> delivery path, walked
+// hop by hop) are the lowest-priority job. `alive` counts running workers (incremented at start,
+// decremented at every exit), so the planner stops waiting within a millisecond when there are
+// none. Termination: the planner sets `stop` when it leaves (also for a host round trip); workers
+// then drain the needed queue and exit; an idle worker also exits after 5 s, and on the host
+// watchdog's abort word.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "tsw_astar.h"
+#include "tsw_internal.h"
+#include "tsw_plan.h"
+
+namespace tsw {
+
+__device__ __forceinline__ uint32_t w_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool w_cas(uint32_t* p, uint32_t expect, uint32_t want) {
+  return __hip_atomic_compare_exchange_strong(p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+// a worker is one wave of a multi-wave workgroup: order its own memory accesses without s_barrier
+__device__ __forceinline__ void wave_sync() {
+  __threadfence_block();
+  wave_order();
+}
+__device__ __forceinline__ uint32_t hw_xcc_id() {
+  return (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID[3:0]
+}
+
+// lane 0: claim the next pair (0: needed queue, 1: speculative queue, 2: task chain, -1: exit).
+// Task chains (long, lowest priority) only go to workers with take_t: the others stay free for the
+// pairs the planner needs or will need soon.
+__device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags) {
+  const unsigned long long t0 = wall_clock64();
+  // one pass over the queues in priority order: >= 0 claimed (queue id), -1 nothing, -2 stop
+  auto scan = [&]() -> int {
+    for (;;) {
+      const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
+      if (cn < hn) {
+        if (w_cas(&cc->claim_n, cn, cn + 1u)) {
+          *idx = cn;
+          return 0;
+        }
+        continue;
+      }
+      // relaxed poll (an acquire here would invalidate this XCD's L2 on every idle spin)
+      if (w_ld(&cc->stop)) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        // the final needed head was published before `stop`: drain what is left, then exit
+        if (w_ld(&cc->claim_n) < w_ld(&cc->head_n)) continue;
+        return -2;
+      }
+      const uint32_t hs = w_ld(&cc->head_s), cs = w_ld(&cc->claim_s);
+      if (cs < hs) {
+        if (w_cas(&cc->claim_s, cs, cs + 1u)) {
+          *idx = cs;
+          return 1;
+        }
+        continue;
+      }
+      if (take_t) {
+        const uint32_t ht = w_ld(&cc->head_t), ct = w_ld(&cc->claim_t);
+        if (ct < ht) {
+          if (w_cas(&cc->claim_t, ct, ct + 1u)) {
+            *idx = ct;
+            return 2;
+          }
+          continue;
+        }
+      }
+      return -1;
+    }
+  };
+  // Idle: poll only the planner's publish count (one load) and rescan the queues when it moves, or
+  // every 64 polls as a safety net. Idle waves polling every head and claim word kept a few lines of
+  // the fabric hot and slowed the planner's own memory accesses (worse the more workers run).
+  uint32_t seen = w_ld(&cc->pub);
+  for (;;) {
+    const int r = scan();
+    if (r >= 0) return r;
+    if (r == -2) return -1;
+    for (uint32_t k = 0;; ++k) {
+      // host watchdog abort (pinned host memory, read over the host link: rarely)
+      if ((k & 255u) == 255u && hflags &&
+          __hip_atomic_load(&hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+        return -1;
+      if (wall_clock64() - t0 > 500000000ull) return -1;  // 5 s idle: safety exit
+      if (k < 8) __builtin_amdgcn_s_sleep(2);
+      else __builtin_amdgcn_s_sleep(16);
+      const uint32_t p = w_ld(&cc->pub);
+      if (p != seen || (k & 63u) == 63u) {
+        seen = p;
+        break;
+      }
+    }
+  }
+}
+
+// lane 0, non-blocking: claim one pair of the needed or the speculative queue (0 / 1), else -1.
+// A worker walking a task chain calls this between hops, so chains (lowest priority, up to ~100
+// A* each) never hold a worker while pairs the planner needs or will need soon are queued.
+__device__ __forceinline__ int worker_try_claim(CoopCtl* cc, uint32_t* idx) {
+  for (;;) {
+    const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
+    if (cn < hn) {
+      if (w_cas(&cc->claim_n, cn, cn + 1u)) {
+        *idx = cn;
+        return 0;
+      }
+      continue;
+    }
+    const uint32_t hs = w_ld(&cc->head_s), cs = w_ld(&cc->claim_s);
+    if (cs < hs) {
+      if (w_cas(&cc->claim_s, cs, cs + 1u)) {
+        *idx = cs;
+        return 1;
+      }
+      continue;
+    }
+    return -1;
+  }
+}
+
+// global g-score slot tag (k_astar / tier-2 scheme: tag:10 | label:2 | g:20, cleared every 1023)
+__device__ __forceinline__ uint32_t slot_tag(uint32_t* GS, uint32_t ncell, uint32_t& ep, uint32_t lane) {
+  if (ep % 1023u == 0u && ep > 0u)
+    for (uint32_t c = lane; c < ncell; c += 64u) GS[c] = 0u;
+  wave_sync();
+  const uint32_t tag = ep % 1023u + 1u;
+  ++ep;
+  return tag;
+}
+
+// One coop worker = one wave. wid: worker index (its global g-score slot / heap / epoch);
+// wsm: this wave's LDS slice (A.lds_per_wave bytes: heap, then g-scores, then the free bitmap).
+__device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, uint32_t wid) {
+  const DevGrid G = A.G;
+  uint64_t* Hp = wsm;
+  const uint32_t lane = threadIdx.x & 63u, ncell = G.ncell, hcap = A.hcap, gs_lds = A.gs_lds;
+  // a worker on the planner's XCD leaves at once: the planner's agent arrays, occupancy and table
+  // lines then share that XCD's 4 MB L2 with nobody's g-score slots. The planner publishes its XCD
+  // first thing; a worker that does not see it within ~20 us stays.
+  if (A.avoid_xcc) {
+    uint32_t px = 0;
+    for (int k = 0; k < 64 && px == 0u; ++k) {
+      px = w_ld(&A.cc->planner_xcc);
+      if (px == 0u) __builtin_amdgcn_s_sleep(8);
+    }
+    if (px != 0u && px - 1u == hw_xcc_id()) return;  // wave-uniform, before `alive`
+  }
+  uint32_t* GSl = reinterpret_cast<uint32_t*>(wsm + hcap);  // gs_lds == 1
+  uint8_t* GB = reinterpret_cast<uint8_t*>(wsm + hcap);      // gs_lds == 2
+  const uint32_t gsb = gs_lds == 1u ? ncell * 4u : gs_lds == 2u ? (ncell + 15u) / 16u * 16u : 0u;
+  const uint32_t* FB = G.freebits;
+  if (A.stage_fb) {
+    uint32_t* fb = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wsm + hcap) + gsb);
+    const uint32_t nfw = G.H * G.Ww;
+    for (uint32_t t = lane; t < nfw; t += 64u) fb[t] = G.freebits[t];
+    FB = fb;
+  }
+  if (gs_lds == 1u)
+    for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
+  uint32_t* GSg = A.gs_all + (uint64_t)wid * ncell;
+  uint64_t* Hg = A.heaps + (uint64_t)wid * A.ghcap;
+  uint32_t ep = A.epochs[wid], epl = 0;
+  wave_sync();
+  if (lane == 0) __hip_atomic_fetch_add(&A.cc->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // exact A* for (v, goal): tier 1 LDS heap + LDS (or global) g-scores, tier 2 global u32
+  // g-scores, tier 3 global heap (the k_astar_wave -> k_astar hand-off chain, in one wave)
+  auto resolve_exact = [&](uint32_t v, uint32_t goal) -> uint8_t {
+    int32_t L = 0;
+    uint8_t code = NH_UNKNOWN;
+    if (gs_lds == 2u) {
+      uint4* g4 = reinterpret_cast<uint4*>(GB);
+      for (uint32_t c = lane; c < (ncell + 15u) / 16u; c += 64u) g4[c] = make_uint4(0u, 0u, 0u, 0u);
+      wave_sync();
+      code = astar_wave_par<2, false>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr);
+    } else if (gs_lds == 1u) {
+      if (epl % 1023u == 0u && epl > 0u) {
+        for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
+      }
+      wave_sync();
+      const uint32_t tag = epl % 1023u + 1u;
+      ++epl;
+      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr);
+    } else {
+      const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
+      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr);
+    }
+    if (L == -2 && gs_lds != 0u) {
+      const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
+      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr);
+    }
+    if (L == -2) {
+      const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
+      if (lane == 0) code = astar_one(G, v, goal, tag, Hg, A.ghcap, GSg, &L, &A.cc->err);
+      code = (uint8_t)__builtin_amdgcn_readfirstlane(code);
+    }
+    return code;
+  };
+  uint32_t cur_q = 0;  // queue of the query being resolved (0 needed, 1 spec, 2 chain)
+  auto resolve = [&](uint32_t v, uint32_t goal) -> uint8_t {
+    const unsigned long long tr0 = wall_clock64();
+    const uint8_t code = resolve_exact(v, goal);
+    if (lane == 0) {
+      __hip_atomic_fetch_add(&A.cc->wbusy[cur_q], wall_clock64() - tr0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&A.cc->wcount[cur_q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return code;
+  };
+  // the code (or NH_UNKNOWN after a global-heap overflow, flagged in cc->err): an agent-scope
+  // store the planner's polling load sees
+  auto publish_code = [&](uint32_t v, int32_t tab, uint8_t code, bool chain) {
+    if (lane == 0 && tab >= 0) {
+      __hip_atomic_store(A.nh + (uint64_t)tab * A.nstride + v, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&A.cc->worker_queries, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (chain) __hip_atomic_fetch_add(&A.cc->chain_queries, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  auto code_at = [&](uint32_t v, int32_t tab) -> uint8_t {  // current code, past stale caches
+    const uint8_t* p = A.nh + (uint64_t)tab * A.nstride + v;
+    const uint32_t w = w_ld(reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u));
+    return (uint8_t)(w >> (8u * (uint32_t)((uintptr_t)p & 3u)));
+  };
+  const bool take_t = (wid & A.tmask) == A.tmask;
+  for (;;) {
+    int which = -1;
+    uint32_t idx = 0;
+    if (lane == 0) which = worker_claim(A.cc, &idx, take_t, A.hflags);
+    which = __builtin_amdgcn_readfirstlane(which);
+    if (which < 0) break;
+    idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+    // the entry was published by the planner's release of the head (or by the host before the
+    // launch): read it past stale caches
+    const uint32_t* e = reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : A.QT) + idx);
+    const uint32_t v = w_ld(e), goal = w_ld(e + 1);
+    const int32_t tab = (int32_t)w_ld(e + 2);
+    cur_q = (uint32_t)which;
+    if (which < 2) {
+      publish_code(v, tab, resolve(v, goal), false);
+      continue;
+    }
+    // task chain: the path an agent carrying this task walks from its pickup to the delivery
+    // (every hop is get_path(cell, delivery)[1], tswap.rs:263-266): follow resolved codes and
+    // resolve each unresolved hop in turn; stop at a pair someone else has queued, at a stay code,
+    // or at the goal. Pairs are not marked pending, so an abandoned chain leaves nothing behind.
+    if (tab < 0) continue;
+    uint32_t c = v;
+    for (uint32_t hop = 0; hop < ncell && c != goal; ++hop) {
+      // the planner is done: abandon the rest of the chain (nothing is marked pending)
+      if ((uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? w_ld(&A.cc->stop) : 0u)) break;
+      // pairs the planner queued meanwhile come first (A.preempt)
+      while (A.preempt) {
+        int w2 = -1;
+        uint32_t i2 = 0;
+        if (lane == 0) w2 = worker_try_claim(A.cc, &i2);
+        w2 = __builtin_amdgcn_readfirstlane(w2);
+        if (w2 < 0) break;
+        i2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i2);
+        const uint32_t* e2 = reinterpret_cast<const uint32_t*>((w2 == 0 ? A.QN : A.QS) + i2);
+        const uint32_t v2 = w_ld(e2), g2 = w_ld(e2 + 1);
+        const int32_t t2 = (int32_t)w_ld(e2 + 2);
+        cur_q = (uint32_t)w2;
+        publish_code(v2, t2, resolve(v2, g2), false);
+        cur_q = 2u;
+      }
+      uint8_t code = (uint8_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(c, tab) : 0u);
+      if (code == NH_UNKNOWN) {
+        code = resolve(c, goal);
+        publish_code(c, tab, code, true);
+      }
+      if (code >= NH_STAY) break;  // stay (unreachable goal), pending elsewhere, or overflow
+      c = step_cell(c, code, G.W);
+    }
+  }
+  if (lane == 0) {
+    A.epochs[wid] = ep;
+    // every exit path after the increment: the planner's "no worker left" test reads this
+    __hip_atomic_fetch_sub(&A.cc->alive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+}  // namespace tsw

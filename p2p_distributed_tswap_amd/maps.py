@@ -267,6 +267,14 @@ def c5_instance(n_agents: int = 10000, n_tasks: int = 10000, seed: int = 0x1024)
     return rows, starts, tasks
 
 
+def wh10k_instance(n_agents: int = 10000, n_tasks: int = 30000, seed: int = 0x510220):
+    """The north_star's "10k-agent warehouse": the warehouse generator at 510x220 (shelf blocks,
+    1-wide aisles), 10,000 agents, 30,000-task MAPD stream. Returns (rows, starts, tasks)."""
+    rows = warehouse_map(510, 220, seed)
+    starts, tasks = make_instance(rows, n_agents, n_tasks, seed)
+    return rows, starts, tasks
+
+
 CONFIGS = {
     # name: (map factory, n_agents, n_tasks, instance seed)  — BASELINE.json configs
     "c1_bundled_10": (bundled_map, 10, 30, 1),

@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 
 
 class _env:
-    """Kernel selection is read when a context is created (TSW_BFS_KERNEL, TSW_BFS_LISTCAP)."""
+    """Kernel selection is read when a context of the DIAGNOSTIC build is created (TSW_BFS_KERNEL,
+    TSW_BFS_LISTCAP, ...); the production library reads no environment and runs its default chain."""
 
     def __init__(self, **kv):
         self.kv = kv
@@ -51,7 +52,7 @@ GRIDS = {
 def _check(rows, goals, **env):
     cells = maps.rows_to_array(rows)
     og = OracleGraph(cells)
-    with _env(**env), Planner(rows) as p:
+    with _env(**env), Planner(rows, diag=bool(env)) as p:
         got = p.dist_tables(goals)
     for k, g in enumerate(goals):
         ref = og.bfs(int(g))
@@ -66,11 +67,14 @@ def _goals(rows, n, seed):
     return rng.choice(free, size=min(n, free.size), replace=False).astype(np.uint32)
 
 
-@pytest.mark.parametrize("kernel", ["blk", "wave", "block", "big"])
+@pytest.mark.parametrize("kernel", ["default", "blk", "wave", "block", "big"])
 @pytest.mark.parametrize("name", sorted(GRIDS))
 def test_bfs_kernels_bit_exact(kernel, name):
     rows = GRIDS[name]()
-    _check(rows, _goals(rows, 40, 7), TSW_BFS_KERNEL=kernel)
+    if kernel == "default":  # the production library's own kernel choice
+        _check(rows, _goals(rows, 40, 7))
+    else:
+        _check(rows, _goals(rows, 40, 7), TSW_BFS_KERNEL=kernel)
 
 
 @pytest.mark.parametrize("name", sorted(GRIDS))
@@ -161,7 +165,7 @@ def test_bfs_den520d_full_size(kernel):
     goals = np.sort(_goals(rows, 1000, 0x520D))
     ncell = 256 * 257
     env = dict(TSW_BFS_KERNEL="blk", TSW_BFS_PAIR=1) if kernel == "blk-pair" else dict(TSW_BFS_KERNEL=kernel)
-    with _env(**env), Planner(rows) as p:
+    with _env(**env), Planner(rows, diag=True) as p:
         buf = _DevBuf(goals.size * ncell * 2)
         p.dist_tables_device(goals, buf.ptr.value)
         got = buf.to_host(np.empty((goals.size, ncell), dtype=np.uint16))
@@ -178,9 +182,31 @@ def test_bfs_symmetry_full_goal_set(kernel):
     rows = maps.cave_map(96, 97, 0x5EED)
     cells = maps.rows_to_array(rows).reshape(-1)
     free = np.flatnonzero(cells != ord("@")).astype(np.uint32)
-    with _env(TSW_BFS_KERNEL=kernel), Planner(rows) as p:
+    with _env(TSW_BFS_KERNEL=kernel), Planner(rows, diag=True) as p:
         t = p.dist_tables(free)
     sub = t[:, free].astype(np.int64)
     assert np.array_equal(sub, sub.T)
     assert np.all(t[:, cells == ord("@")] == 0xFFFF)
     assert np.all(t[np.arange(free.size), free] == 0)
+
+
+def test_bfs_den520d_10k_goals_as_benched():
+    """the exact launch bench.py times — 10,000 distinct den520d goals (configs[3]) in
+    one tsw_dist_tables_device call of the production library — every table's sha1 against the
+    oracle's (tests/golden/tables_den520d_10k.npz, made by make_digests.py den520d_10k)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_digests import den520d_goals, table_digests
+
+    ref = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tables_den520d_10k.npz"))
+    rows, goals = den520d_goals(10000)
+    assert np.array_equal(goals, ref["goals"])
+    ncell = 256 * 257
+    with Planner(rows) as p:
+        buf = _DevBuf(goals.size * ncell * 2)
+        p.dist_tables_device(goals, buf.ptr.value)
+        got = buf.to_host(np.empty((goals.size, ncell), dtype=np.uint16))
+    dig = table_digests(got)
+    bad = np.flatnonzero(dig != ref["sha1_8"])
+    assert bad.size == 0, f"{bad.size} of {goals.size} tables differ, first goal {goals[bad[0]]}"

@@ -2,7 +2,7 @@
 import numpy as np
 import pytest
 
-from p2p_distributed_tswap_amd import Planner, TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP, maps
+from p2p_distributed_tswap_amd import Planner, TSW_F_EAGER_NEXTHOP, TSW_F_EXIT_MODE, TSW_F_LAZY_NEXTHOP, maps
 from oracle import OracleGraph
 
 pytestmark = pytest.mark.gpu
@@ -92,7 +92,7 @@ def test_astar_wave_heap_overflow_handoff(monkeypatch, name):
     s = rng.choice(free, 200).astype(np.uint32)
     g = rng.choice(free, 200).astype(np.uint32)
     monkeypatch.setenv("TSW_ASTAR_WAVE_HCAP", "16")
-    with Planner(rows) as p:
+    with Planner(rows, diag=True) as p:
         nxt, ln = p.get_path_next(s, g)
     for q in range(s.size):
         rn, rl, _ = og.get_path_next(int(s[q]), int(g[q]))
@@ -223,7 +223,7 @@ def test_mapd_occ_placement(split, monkeypatch):
     starts, tasks = maps.make_instance(rows, 400, 1200, 0x400)
     og = OracleGraph(maps.rows_to_array(rows))
     ref, rgoal = og.mapd(starts, tasks, 150, trace_goals=True)
-    with Planner(rows) as p:
+    with Planner(rows, diag=True) as p:
         rec, goal = p.plan_mapd_arrays(starts, tasks, 150, trace_goals=True)
     assert np.array_equal(goal, rgoal)
     assert np.array_equal(rec, ref)
@@ -298,7 +298,7 @@ def test_astar_wave_cores_and_tiers(monkeypatch, mode):
     right = free[(free % W) > W - 20]
     s = np.concatenate([rng.choice(left, 48), rng.choice(free, 16)]).astype(np.uint32)
     g = np.concatenate([rng.choice(right, 48), rng.choice(free, 16)]).astype(np.uint32)
-    with Planner(rows) as p:
+    with Planner(rows, diag=mode != "coop") as p:
         nxt, ln = p.get_path_next(s, g)
     for q in range(s.size):
         rn, rl, _ = og.get_path_next(int(s[q]), int(g[q]))
@@ -320,7 +320,7 @@ def test_astar_wave_batch_gscore_placement(monkeypatch, gs):
     nq = 3000
     s = rng.choice(free, nq).astype(np.uint32)
     g = rng.choice(free, nq).astype(np.uint32)
-    with Planner(rows) as p:
+    with Planner(rows, diag=gs != "auto") as p:
         nxt, ln = p.get_path_next(s, g)
     bad = [q for q in range(nq) if (nxt[q], ln[q]) != og.get_path_next(int(s[q]), int(g[q]))[:2]]
     assert not bad, f"{len(bad)} mismatches ({gs}), first {bad[:5]}"
@@ -342,3 +342,46 @@ def test_astar_lds_more_queries_than_slots():
     idx = np.concatenate([np.arange(0, nq, 7), np.arange(65536, nq)])  # surplus checked in full
     bad = [int(q) for q in idx if (nxt[q], ln[q]) != og.get_path_next(int(s[q]), int(g[q]))[:2]]
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
+def _plan_vs_oracle(rows, starts, tasks, max_t, **kw):
+    og = OracleGraph(maps.rows_to_array(rows))
+    ref, rgoal = og.mapd(starts, tasks, max_t, trace_goals=True)
+    with Planner(rows, **kw) as p:
+        rec, goal = p.plan_mapd_arrays(starts, tasks, max_t, trace_goals=True)
+        st = p.stats()
+    assert rec.shape == ref.shape
+    if not np.array_equal(goal, rgoal):
+        t = int(np.argmax((goal != rgoal).any(axis=0)))
+        pytest.fail(f"goal divergence first at t={t}")
+    assert np.array_equal(rec, ref)
+    return st
+
+
+@pytest.mark.parametrize("name,n,m,seed,max_t", [("rand32", 200, 600, 0x3232, 2000), ("warehouse", 1000, 3000, 0x170084, 120)])
+def test_mapd_exit_mode(name, n, m, seed, max_t):
+    """the exit mode (TSW_F_EXIT_MODE: lazy next hops resolved by host-launched K3 passes
+    at planner exits, no concurrent workers) on lazy configs, bit-exact; the C3 warehouse prefix
+    exercises the speculative queue leftovers resolved at the end of the call."""
+    rows = _grid(name)
+    starts, tasks = maps.make_instance(rows, n, m, seed)
+    st = _plan_vs_oracle(rows, starts, tasks, max_t, flags=TSW_F_LAZY_NEXTHOP | TSW_F_EXIT_MODE)
+    assert st["coop_workers"] == 0 and sum(st["plan_exits"]) > 0
+
+
+def test_mapd_watchdog_fallback_mid_plan():
+    """the watchdog fallback. A 1 ms watchdog fires during the C3 plan (one step of 1,000
+    agents' assignment already takes longer): the coop plan gives up its waits, the workers leave, the
+    call resumes in exit mode from the returned PlanCtl, and the plan stays bit-exact."""
+    rows, starts, tasks = maps.config_instance("c3_warehouse_170x84")
+    st = _plan_vs_oracle(rows, starts, tasks, 150, watchdog_ms=1)
+    assert st["watchdog_fires"] >= 1
+
+
+def test_mapd_coop_workers_in_plan_dispatch():
+    """The C3 prefix in coop mode: the plan dispatch carries its K3 workers (coop_workers > 0), the
+    planner never leaves the kernel for K3 (no exits), the workers report busy time; bit-exact."""
+    rows, starts, tasks = maps.config_instance("c3_warehouse_170x84")
+    st = _plan_vs_oracle(rows, starts, tasks, 150)
+    assert st["coop_workers"] > 0 and st["walker_launches"] == 1 and sum(st["plan_exits"]) == 0
+    assert st["coop_worker_busy_ms"][0] + st["coop_worker_busy_ms"][1] > 0 and st["watchdog_fires"] == 0

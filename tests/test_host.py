@@ -44,8 +44,34 @@ def test_no_cpu_fallback_without_gpu():
 
 def test_missing_library_raises(tmp_path):
     with pytest.raises(pkg.TswapError):
-        pkg._lib = None
         pkg.load_library(str(tmp_path / "nope.so"))
+
+
+def test_production_library_reads_no_environment():
+    """the wrong-answer diagnostic switches (TSW_BFS_DBG ...) and every A/B knob exist
+    only in the diagnostic build; the production library contains no TSW_* variable name and no
+    getenv call, so a caller's environment cannot change a result."""
+    if not os.path.exists(pkg.LIB_PATH):
+        pytest.skip("libtswap_hip.so not built")
+    blob = open(pkg.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"TSW_[A-Z0-9_]+", blob))
+    assert not names, sorted(names)
+    assert b"getenv" not in blob
+    if os.path.exists(pkg.DIAG_LIB_PATH):
+        assert b"TSW_BFS_DBG" in open(pkg.DIAG_LIB_PATH, "rb").read()
+
+
+def test_header_documents_every_option():
+    """Every tsw_opts field and TSW_F_* flag is documented in include/tswap.h and mirrored in Python."""
+    txt = open(os.path.join(ROOT, "include", "tswap.h")).read()
+    body = txt[txt.index("typedef struct {\n    int32_t device;"):txt.index("} tsw_opts;")]
+    fields = re.findall(r"\b(?:int32_t|uint32_t|uint64_t)\s+([a-z_]+);", body)
+    assert fields == [f for f, _ in pkg._Opts._fields_]
+    for line in body.splitlines():
+        if re.search(r"\b(?:int32_t|uint32_t|uint64_t)\s+[a-z_]+;", line) and "reserved" not in line:
+            assert "/*" in line, line
+    flags = dict((k, int(v.rstrip("u"))) for k, v in re.findall(r"#define (TSW_F_[A-Z_]+) (\d+u)", txt))
+    assert flags == {k: getattr(pkg, k) for k in flags} and len(flags) == 3
 
 
 def test_grid_to_bytes_ragged():
