@@ -17,7 +17,9 @@ Extra objects on the line:
   roofline      the kernel class with the most device time inside the timed steps (HIP events
                 on the library's stream, tsw_get_stats), algorithmic bytes per launch, and the
                 PMC traffic per launch from profiles/<PROFILE_TAG>/pmc.json — only when that file
-                was measured on THIS workload (same algorithmic bytes per launch), else null.
+                was measured on THIS workload (same algorithmic bytes per launch), else null. The
+                plan dispatch (k_plan) carries the planner AND its exact-A* workers (coop mode): its
+                algorithmic bytes are 46 B per agent-step plus 17 B per worker query.
   latency       k_plan against its latency floor (bound "latency"): rules / movement rounds x the
                 measured floor per round shape (tsw_probe_round_floors), beside the achieved section
                 time; the K3 wait time (the A* critical path) beside it. DESIGN.md "Latency roofline".
@@ -25,7 +27,12 @@ Extra objects on the line:
                 cells/s and fraction of the 8 TB/s HBM peak (algorithmic bytes).
   cpu_baseline  the oracle (faithful single-thread C restatement of tswap.rs) planning a bounded
                 prefix of the same instance on one pinned host core, rank 0 only; its prefix is
-                also compared bit-exactly with the GPU plan.
+                also compared bit-exactly with the GPU plan, and the GPU plans the SAME prefix
+                (same max_t, from an empty table store) for a like-for-like rate.
+  sharded_plan  N > 1 only: the north_star multi-GPU pipeline on rank 0's instance — every rank
+                builds its goal shard of the plan's K1 tables, RCCL all-gather over xGMI, rank 0
+                imports them into its planning context and plans (max over ranks of the whole
+                pipeline), bit-exact against rank 0's replica plan.
 """
 from __future__ import annotations
 
@@ -41,7 +48,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md ("HBM: 8 TB/s peak")
-PROFILE_TAG = "r2"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
+PROFILE_TAG = "r3"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
 BFS_WORKLOAD = "bfs:den520d_10k"
 
 
@@ -142,7 +149,7 @@ def host_cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(rows, starts, tasks, n_agents, steps, gpu_rec):
+def cpu_baseline(rows, starts, tasks, n_agents, steps, gpu_rec, gpu_prefix=None):
     """The C oracle (single thread, -O2) planning the first `steps` timesteps of the same instance,
     pinned to one host core (sched_setaffinity = taskset -c <core>), compared with the GPU plan."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -171,8 +178,80 @@ def cpu_baseline(rows, starts, tasks, n_agents, steps, gpu_rec):
         "host_cores_total": os.cpu_count(),
         "host_cores_allowed": len(old),
         "prefix_bit_exact_vs_gpu": bool(gpu_rec is not None and np.array_equal(rec, gpu_rec[:, :T])),
+        # the GPU timed on the same sample (same instance, same max_t, empty table store),
+        # so the CPU/GPU ratio compares the same work; the headline value covers the full horizon
+        "gpu_same_sample": gpu_prefix,
+        "gpu_over_cpu_same_sample": (round(gpu_prefix["agent_steps_per_s"] / (n_agents * T / tcd), 1)
+                                     if gpu_prefix else None),
         "note": ("a C port with dense stamped arrays (no HashMap) and the Rust std BinaryHeap restated: "
                  "likely faster than the Rust original, so the GPU/CPU ratio is conservative"),
+    }
+
+
+def goal_set(rows, starts, tasks) -> np.ndarray:
+    """The closed goal set of a MAPD instance (start cells, pickups, deliveries: goals only move
+    between agents by rule 3/4, tswap.rs:198-249), as sorted cell ids."""
+    w = len(rows[0])
+    c = np.concatenate([starts[:, 1] * w + starts[:, 0], tasks[:, 1] * w + tasks[:, 0], tasks[:, 3] * w + tasks[:, 2]])
+    return np.unique(c.astype(np.uint32))
+
+
+def sharded_plan_leg(args, rows, n_agents, n_tasks, seed, rank, world, dev, dist, barrier, allmax, ref_rec):
+    """north_star multi-GPU pipeline: rank 0's instance planned with its goal tables
+    built goal-sharded on all ranks (K1 into a torch tensor, tsw_dist_tables_device), RCCL
+    all-gather over xGMI (sharding.build_and_allgather), tsw_import_tables_device into rank 0's
+    PLANNING context, then tsw_plan_mapd there — all inside the timed region, max over ranks. The
+    step itself does not shard: the other ranks only build and send tables."""
+    import torch
+
+    from p2p_distributed_tswap_amd import Planner, maps, sharding
+
+    starts, tasks = maps.make_instance(rows, n_agents, n_tasks, seed)  # rank 0's replica instance
+    goals = goal_set(rows, starts, tasks)
+    ncell = len(rows) * len(rows[0])
+    p = Planner(rows, device=dev)
+    build = lambda g, o: p.dist_tables_device(g, o.data_ptr())  # noqa: E731
+    times, parts, rec = [], [], None
+    for rep in range(max(args.steps, 1) + 1):  # first repetition = warm-up
+        p.clear_tables()
+        p.reset_stats()
+        barrier()
+        t0 = time.perf_counter()
+        full = sharding.build_and_allgather(goals, ncell, rank, world, build, dist, "cuda")
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if rank == 0:
+            p.reset_stats()  # from here on: the planning context's own work (imports + plan)
+            for _, gl, off in sharding.gathered_blocks(goals, world):
+                if gl.size:
+                    p.import_tables_device(gl, full[off:off + gl.size].data_ptr())
+            t2 = time.perf_counter()
+            rec, _ = p.plan_mapd_arrays(starts, tasks, 2000)
+            t3 = time.perf_counter()
+        else:
+            t2 = t3 = t1
+        del full
+        barrier()
+        dt = allmax(time.perf_counter() - t0)
+        if rep > 0:
+            times.append(dt)
+            parts.append((t1 - t0, t2 - t1, t3 - t2))
+    st = p.stats()  # rank 0: the last repetition's import + plan
+    p.close()
+    if rank != 0:
+        return None
+    n = len(times)
+    return {
+        "instance": f"{args.config} seed {seed} (rank 0's replica)",
+        "goals": int(goals.size), "goals_per_rank": int(sharding.shard_rows(goals.size, world)),
+        "sharded_plan_ms": round(1e3 * sum(times) / n, 3),
+        "k1_shard_build_allgather_ms": round(1e3 * sum(x[0] for x in parts) / n, 3),
+        "import_ms": round(1e3 * sum(x[1] for x in parts) / n, 3),
+        "plan_ms": round(1e3 * sum(x[2] for x in parts) / n, 3),
+        "agent_steps_per_s": round(n_agents * rec.shape[1] / (sum(times) / n), 1),
+        "planning_context_k1_goals": int(st["bfs_goals"]),  # 0: every table came from the all-gather
+        "bit_exact_vs_replica_plan": bool(ref_rec is not None and rank == 0 and np.array_equal(rec, ref_rec)),
+        "backend": args.dist_backend,
     }
 
 
@@ -249,23 +328,41 @@ def main():
         # latency floors of k_plan's round shapes on its own workgroup size (tsw_probe.hip), measured
         # after the timed region
         us_wave, us_pass = planner.probe_round_floors(0)
+        gpu_prefix = None
+        if rank == 0 and not args.no_cpu:
+            # the CPU baseline's sample on the GPU (outside the timed region)
+            planner.clear_tables()
+            torch.cuda.synchronize()
+            tp = time.perf_counter()
+            prec, _ = planner.plan_mapd_arrays(starts, tasks, args.cpu_steps)
+            tpd = time.perf_counter() - tp
+            gpu_prefix = {"timesteps": int(prec.shape[1]), "s": round(tpd, 4),
+                          "agent_steps_per_s": round(n_agents * prec.shape[1] / tpd, 1),
+                          "bit_exact_vs_full_plan": bool(np.array_equal(prec, last_rec[:, :prec.shape[1]]))}
         planner.close()
 
         # kernel classes inside the timed region (device time from HIP events on the library stream)
         steps_total = st["steps"]
+        # K3 in coop mode runs INSIDE the plan dispatch (workgroups 1.. of k_plan): its time is the
+        # workers' A* busy time summed over worker waves (wave-ms, overlapping the dispatch), plus any
+        # host-launched K3 passes (exit mode / eager tables: HIP events)
+        worker_wave_ms = float(sum(st["coop_worker_busy_ms"]))
         cats = {
-            "K3": ("k_astar_wave / k_astar_lds / k_astar (exact A* next hop, get_path tswap.rs:288-390)",
-                   st["astar_ms"], st["astar_launches"],
-                   # per pass: every query read (16 B) + its next-hop code written (1 B)
+            "K3": ("exact A* next hop (get_path tswap.rs:288-390): coop workers inside the plan dispatch "
+                   "+ host-launched k_astar_wave / k_astar_lds / k_astar passes",
+                   st["astar_ms"] + worker_wave_ms, st["astar_launches"],
+                   # every query read (16 B) + its next-hop code written (1 B)
                    17.0 * st["astar_queries"] / max(st["astar_launches"], 1)),
-            "k_plan": ("k_plan (K2 tswap_step + K4 assignment, persistent, tswap.rs:104-286)",
+            "k_plan": ("k_plan dispatch (K2 tswap_step + K4 assignment, persistent planner, tswap.rs:104-286; "
+                       "with its coop K3 workers)",
                        st["walker_ms"], st["walker_launches"],
-                       # ~46 B per agent-step
-                       46.0 * n_agents * steps_total / max(st["walker_launches"], 1)),
+                       # ~46 B per agent-step, + 17 B per query the in-dispatch workers ran
+                       (46.0 * n_agents * steps_total + 17.0 * st["astar_queries"]) / max(st["walker_launches"], 1)),
             "K1": ("k_bfs_blk + k_classify (BFS tables + next-hop codes)", st["bfs_ms"], st["bfs_launches"],
                    bfs_bytes_per_goal(w, h, True) * st["bfs_goals"] / max(st["bfs_launches"], 1)),
         }
-        dom = max(cats, key=lambda k: cats[k][1])
+        # the dominant kernel: the most DEVICE time (dispatch-level; K3's wave-ms overlap k_plan)
+        dom = max(("k_plan", "K1") + (("K3",) if worker_wave_ms == 0.0 else ()), key=lambda k: cats[k][1])
         name, dom_ms, dom_launches, per_launch_bytes = cats[dom]
         avg_launch_ms = dom_ms / max(dom_launches, 1)
         achieved = per_launch_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
@@ -285,11 +382,22 @@ def main():
             # every kernel class of the timed plans (scripts/summarize_profile.py pairs these with PMC)
             "classes": {k: {"device_ms": round(v[1], 3), "launches": int(v[2]),
                             "algorithmic_bytes_per_launch": round(v[3], 1)} for k, v in cats.items()},
+            "k3_workers": {"waves": int(st["coop_workers"]), "busy_wave_ms": round(worker_wave_ms, 3),
+                           "busy_wave_ms_by_queue": {q: round(x, 3) for q, x in
+                                                     zip(("needed", "speculative", "task_chains"),
+                                                         st["coop_worker_busy_ms"])},
+                           "note": "K3 device_ms = these busy wave-ms (workers run inside the k_plan dispatch) "
+                                   "+ host-launched K3 passes"},
             "note": ("K3 and k_plan move a few bytes per serial heap / commit step: their HBM fraction is tiny by "
                      "construction and their binding limit is latency (see `latency`). K1 (bfs.roofline) is the "
                      "HBM-bound kernel." if dom != "K1" else None),
         }
         latency = latency_roofline(st, us_wave, us_pass)
+
+    sharded = None
+    if world > 1 and not args.no_plan:
+        sharded = sharded_plan_leg(args, rows, n_agents, n_tasks, seed, rank, world, dev, dist, barrier, allmax,
+                                   last_rec)
 
     # K1 BFS alone, den520d-like, 10k distinct goals (configs[3]); rank-local shard of the goals
     bfs = None
@@ -365,7 +473,7 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu and not args.no_plan:
-        cpu = cpu_baseline(rows, starts, tasks, n_agents, args.cpu_steps, last_rec)
+        cpu = cpu_baseline(rows, starts, tasks, n_agents, args.cpu_steps, last_rec, gpu_prefix)
 
     if rank == 0:
         line = {
@@ -391,6 +499,7 @@ def main():
             "latency": latency,
             "bfs": bfs,
             "cpu_baseline": cpu,
+            "sharded_plan": sharded,
             "kernel_stats": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
         }
         print(json.dumps(line), flush=True)

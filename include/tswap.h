@@ -22,8 +22,12 @@
  * would keep going — each returns an error code, never a wrong answer:
  *   - grid: at most 2048 cells per side and 2^20 cells      (tsw_create -> NULL)
  *   - BFS distances are u16: a goal whose farthest reachable cell is more than
- *     65534 steps away fails K1 with TSW_EOVERFLOW (only possible on grids of
- *     more than 65535 free cells, e.g. a serpentine 1024x1024 maze)
+ *     65534 steps away (only possible on grids of more than 65535 free cells,
+ *     e.g. a serpentine maze) has no distance table. Planning entry points
+ *     (tsw_plan_mapd, tsw_step, tsw_decide, tsw_next_hop_tables) keep such a goal
+ *     WITHOUT a table and resolve every next hop toward it with the exact A*
+ *     (K3, 20-bit g): same results, slower. The table-returning entry points
+ *     (tsw_dist_tables*, tsw_next_hop_tables_device) return TSW_EOVERFLOW for it.
  *   - exact A*: the LDS-heap kernels hand queries with g >= 2^15, f >= 2^17 or
  *     a heap past their LDS capacity to the global-heap kernel (20-bit g, enough
  *     for any path on a 2^20-cell grid); its heap holds min(4*cells+8, 65536)
@@ -184,8 +188,11 @@ int tsw_next_hop_tables(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint8_t
 /* Goal-sharded K3: the fully resolved next-hop codes of k goals into
  * caller-owned DEVICE memory (k*w*h bytes, row-major, codes as tsw_next_hop_tables). Builds the
  * goals' tables if needed and resolves every multi-candidate cell with the exact A* (eager,
- * whatever the context's next-hop policy): one rank's share of an all-gathered code table. */
-int tsw_next_hop_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint8_t *dev_out);
+ * whatever the context's next-hop policy): one rank's share of an all-gathered code table.
+ * dev_dist (may be NULL): also receives the goals' K1 distance tables (k*w*h u16), so one K1 build
+ * serves both all-gathers. */
+int tsw_next_hop_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint8_t *dev_out,
+                               uint16_t *dev_dist);
 
 /* Ingest k tables AND their next-hop codes (DEVICE memory: k*w*h u16 + k*w*h u8, e.g. the
  * all-gather of tsw_dist_tables_device / tsw_next_hop_tables_device shards): steps then need
@@ -234,6 +241,7 @@ typedef struct {
      * [0] needed pairs, [1] speculative prefetches, [2] task chains */
     double coop_worker_busy_ms[3];
     uint64_t watchdog_fires;    /* plan calls the host watchdog moved to exit mode */
+    uint64_t tableless_goals;   /* goals held without a distance table (u16 overflow; next hops by K3) */
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

@@ -97,7 +97,7 @@ class Stats(ctypes.Structure):
         ("relabels_full", ctypes.c_uint64), ("relabels_inc", ctypes.c_uint64),
         ("move_rounds", ctypes.c_uint64), ("plan_block", ctypes.c_uint32),
         ("coop_workers", ctypes.c_uint32), ("coop_worker_busy_ms", ctypes.c_double * 3),
-        ("watchdog_fires", ctypes.c_uint64),
+        ("watchdog_fires", ctypes.c_uint64), ("tableless_goals", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -148,7 +148,7 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_import_tables_device.argtypes = [vp, P(u32), u32, vp]
     lib.tsw_clear_tables.argtypes = [vp]
     lib.tsw_next_hop_tables.argtypes = [vp, P(u32), u32, P(ctypes.c_uint8)]
-    lib.tsw_next_hop_tables_device.argtypes = [vp, P(u32), u32, vp]
+    lib.tsw_next_hop_tables_device.argtypes = [vp, P(u32), u32, vp, vp]
     lib.tsw_import_next_hops_device.argtypes = [vp, P(u32), u32, vp, vp]
     lib.tsw_get_stats.argtypes = [vp, P(Stats)]
     lib.tsw_reset_stats.argtypes = [vp]
@@ -335,10 +335,12 @@ class Planner:
                                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return out
 
-    def next_hop_tables_device(self, goals, dev_ptr: int):
-        """Resolved next-hop codes of `goals` (eager A*) into device memory (len(goals) x w*h u8)."""
+    def next_hop_tables_device(self, goals, dev_ptr: int, dist_ptr: int = 0):
+        """Resolved next-hop codes of `goals` (eager A*) into device memory (len(goals) x w*h u8);
+        dist_ptr (optional): their K1 distance tables too (len(goals) x w*h u16)."""
         g = np.ascontiguousarray(goals, dtype=np.uint32)
-        self._check(self._lib.tsw_next_hop_tables_device(self._ctx, _u32p(g), g.size, ctypes.c_void_p(dev_ptr)))
+        self._check(self._lib.tsw_next_hop_tables_device(self._ctx, _u32p(g), g.size, ctypes.c_void_p(dev_ptr),
+                                                         ctypes.c_void_p(dist_ptr or None)))
 
     def import_next_hops_device(self, goals, dist_ptr: int, nh_ptr: int):
         """Ingest tables + next-hop codes from device memory (e.g. an all-gather of rank shards)."""

@@ -186,6 +186,7 @@ __global__ void __launch_bounds__(1024) k_bfs_wave(WaveBfsArgs A) {
     while (ncur != 0u) {
       if (lvl >= 0xFFFFu) {
         if (lane == 0) atomicOr(A.err, ERR_DIST_OVERFLOW);
+        if (lane == 0 && A.govf) A.govf[gi] = 1u;  // planned without a table (K3)
         break;
       }
       const uint32_t nxt = cur ^ 1u;

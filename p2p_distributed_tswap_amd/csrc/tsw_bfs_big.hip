@@ -192,6 +192,7 @@ __global__ void __launch_bounds__(512) k_bfs_big(BigBfsArgs A) {
       if (ncur == 0u) break;
       if (lvl >= 0xFFFFu) {
         if (tid == 0) atomicOr(A.err, ERR_DIST_OVERFLOW);
+        if (tid == 0 && A.govf) A.govf[gi] = 1u;  // planned without a table (K3)
         break;
       }
       if (tid == 0) s_cnt[(lvl + 1u) % 3u] = 0u;  // the counter of the level after next

@@ -337,6 +337,8 @@ __global__ void __launch_bounds__(1024) k_bfs_blk(BlkBfsArgs A) {
     while (PAIR ? __ballot(ncur != 0u) != 0ull : ncur != 0u) {
       if (lvl >= 0xFFFFu) {
         if (lane == 0) atomicOr(A.err, ERR_DIST_OVERFLOW);
+        // this goal's table cannot hold its distances (u16): the host plans it without one (K3)
+        if (A.govf && (lane & 31u) == 0u && live) A.govf[gi] = 1u;
         break;
       }
       const uint32_t nxt = cur ^ 1u;

@@ -160,6 +160,12 @@ struct tsw_ctx {
   std::vector<int32_t> h_goal_tab;
   std::vector<uint32_t> h_tab_goal;
   std::vector<uint64_t> h_tab_stamp;  // call counter of the slot's last use (LRU eviction)
+  // 1: the slot's goal is farther than u16 distances reach from some cell (K1 overflow): it is kept
+  // WITHOUT a distance table (all TSW_DIST_INF) and every next hop toward it comes from the exact
+  // A* (K3, 20-bit g) — get_path's usize g-scores (tswap.rs:288-390) have no such limit
+  std::vector<uint8_t> h_tab_tableless;
+  uint8_t* d_govf = nullptr;  // K1 per-goal overflow flags
+  size_t govf_cap = 0;
   std::vector<uint32_t> tab_free;
   uint64_t call_stamp = 0;
   uint64_t table_budget = 0;
@@ -614,7 +620,7 @@ int bfs_prof_print(tsw_ctx* c, const char* name, uint32_t k) {
 // kernel. Next-hop codes (nh != null) come fused from k_bfs, or from k_classify over the
 // finished tables after the wave kernels.
 int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k, uint16_t* dist, uint64_t dstride,
-            uint8_t* nh) {
+            uint8_t* nh, uint8_t* govf = nullptr) {
   if (k == 0) return TSW_OK;
   const bool vec16 = c->G.W % 8u == 0u && dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u;
   const uint32_t max_waves = c->tun.bfs_waves;
@@ -664,6 +670,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     A.wlg = c->d_wlg;
     A.work = &c->d_stat->work;
     A.err = &c->d_stat->err;
+    A.govf = govf;
     A.vec16 = vec16 ? 1u : 0u;
     A.stage = (dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u && !c->tun.bfs_nostage) ? 1u : 0u;
     A.dbg = c->tun.bfs_dbg;
@@ -717,6 +724,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     A.wlg = reinterpret_cast<uint64_t*>(c->d_wlg);
     A.work = &c->d_stat->work;
     A.err = &c->d_stat->err;
+    A.govf = govf;
     A.vec16 = vec16 ? 1u : 0u;
     A.scratch_wgs = (uint32_t)std::min<uint64_t>(c->wave_scratch, c->wlg_waves);
     HIPCHK(hipMemsetAsync(&c->d_stat->work, 0, 4, c->s));
@@ -728,7 +736,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   Timer t(c, CAT_BFS);
   if (nwv == 0) {
     HIPCHK(launch_bfs(c->G, goals, slots, k, dist, dstride, nh, dstride, &c->d_stat->err, c->max_lds, c->num_cu,
-                      c->s));
+                      c->s, govf));
     return TSW_OK;
   }
   TRY(ensure_wave_scratch(c, (uint64_t)c->num_cu * nwv, (size_t)c->npw * 32u, (size_t)c->npw * 2u));
@@ -749,6 +757,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   A.lovf = c->d_lovf;
   A.work = &c->d_stat->work;
   A.err = &c->d_stat->err;
+  A.govf = govf;
   A.vec16 = vec16 ? 1u : 0u;
   A.max_waves = max_waves;
   A.scratch_waves = c->wave_scratch;
@@ -788,6 +797,7 @@ int grow_store(tsw_ctx* c, size_t need) {
   c->tab_cap = (uint32_t)nc;
   c->h_tab_goal.resize(nc, NO_GOAL);
   c->h_tab_stamp.resize(nc, 0);
+  c->h_tab_tableless.resize(nc, 0);
   return TSW_OK;
 }
 
@@ -878,7 +888,10 @@ int finish_tables(tsw_ctx* c, int rc, const std::vector<uint32_t>& newg, const s
   return rc;
 }
 
-int build_new_tables(tsw_ctx* c, const std::vector<uint32_t>& newg, const std::vector<uint32_t>& slots) {
+// tableless_ok: a goal whose distances overflow u16 is registered WITHOUT a table (next hops by K3)
+// instead of failing the call — planning entry points; the table-returning ones pass false.
+int build_new_tables(tsw_ctx* c, const std::vector<uint32_t>& newg, const std::vector<uint32_t>& slots,
+                     bool tableless_ok) {
   std::vector<uint32_t>& lg = c->h_lpt_goals;
   std::vector<uint32_t>& ls = c->h_lpt_slots;
   lg = newg;
@@ -887,23 +900,69 @@ int build_new_tables(tsw_ctx* c, const std::vector<uint32_t>& newg, const std::v
   TRY(ensure_tmp(c, newg.size()));
   HIPCHK(hipMemcpyAsync(c->d_tmp_a, lg.data(), lg.size() * 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipMemcpyAsync(c->d_tmp_b, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, c->s));
-  TRY(run_bfs(c, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh));
+  if (tableless_ok) {
+    if (newg.size() > c->govf_cap || !c->d_govf) {
+      HIPCHK(hipStreamSynchronize(c->s));
+      HIPCHK(dgrow(c->d_govf, c->govf_cap, newg.size()));
+    }
+    HIPCHK(hipMemsetAsync(c->d_govf, 0, newg.size(), c->s));
+  }
+  TRY(run_bfs(c, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh,
+              tableless_ok ? c->d_govf : nullptr));
   c->st.bfs_goals += newg.size();
   c->st.bfs_launches++;
+  for (uint32_t s : slots) c->h_tab_tableless[s] = 0;
+  HIPCHK(hipMemcpyAsync(&c->h_stat->err, &c->d_stat->err, 4, hipMemcpyDeviceToHost, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  if (tableless_ok && c->h_stat->err == ERR_DIST_OVERFLOW) {
+    std::vector<uint8_t> f(newg.size());
+    HIPCHK(hipMemcpy(f.data(), c->d_govf, f.size(), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < f.size(); ++i) {
+      if (!f[i]) continue;
+      const uint32_t slot = ls[i];
+      c->h_tab_tableless[slot] = 1;
+      ++c->st.tableless_goals;
+      // no distance (DAG prefetch reads INF: nothing to follow) and every code unresolved (K3)
+      HIPCHK(hipMemsetAsync(c->d_dist + (size_t)slot * c->tstride, 0xFF, c->tstride * 2, c->s));
+      HIPCHK(hipMemsetAsync(c->d_nh + (size_t)slot * c->tstride, 0xFF, c->tstride, c->s));
+    }
+    HIPCHK(hipMemsetAsync(&c->d_stat->err, 0, 4, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+  }
   return check_err(c);
 }
 
 // Make sure every goal in `goals` (valid free cells) has a table. A failed K1 build (HIP error,
-// distance overflow) leaves no goal registered against a partial table.
-int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in) {
+// distance overflow when !tableless_ok) leaves no goal registered against a partial table.
+int ensure_tables(tsw_ctx* c, const std::vector<uint32_t>& goals_in, bool tableless_ok = false) {
   std::vector<uint32_t> newg, slots;
   newg.reserve(goals_in.size());
   stamp_and_collect(c, goals_in.data(), goals_in.size(), newg);
   if (newg.empty()) return TSW_OK;
   int rc = reserve_slots(c, newg.size(), slots);
-  if (rc == TSW_OK) rc = build_new_tables(c, newg, slots);
+  if (rc == TSW_OK) rc = build_new_tables(c, newg, slots, tableless_ok);
   TRY(finish_tables(c, rc, newg, slots));
-  if (eager_policy(c, newg.size())) TRY(resolve_all_unknown(c, newg, slots));
+  if (eager_policy(c, newg.size())) {
+    // eager resolution over real tables only (a tableless goal stays lazy: one A* per cell would be
+    // a whole-grid search per cell)
+    std::vector<uint32_t> eg, es;
+    for (size_t j = 0; j < newg.size(); ++j)
+      if (!c->h_tab_tableless[slots[j]]) {
+        eg.push_back(newg[j]);
+        es.push_back(slots[j]);
+      }
+    TRY(resolve_all_unknown(c, eg, es));
+  }
+  return TSW_OK;
+}
+
+// TSW_EOVERFLOW if any of `goals` (with tables) is held without one (its distances overflow u16).
+int require_real_tables(tsw_ctx* c, const std::vector<uint32_t>& goals) {
+  for (uint32_t g : goals) {
+    const int32_t t = c->h_goal_tab[g];
+    if (t >= 0 && c->h_tab_tableless[t])
+      RET(TSW_EOVERFLOW, "goal farther than 65534 steps from some cell: no u16 distance table (plans use K3)");
+  }
   return TSW_OK;
 }
 
@@ -1303,7 +1362,7 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   HIPCHK(hipMemcpyAsync(c->d_unused, &m, 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipStreamSynchronize(c->s));  // host vectors above go out of scope only at return, but keep it simple
   TRY(build_occ(c, n));
-  TRY(ensure_tables(c, goalset));
+  TRY(ensure_tables(c, goalset, true));
   TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
   c->qt_count = 0;
   if (c->tun.coop && !eager_policy(c, 0)) {
@@ -1520,7 +1579,7 @@ void tsw_destroy(tsw_ctx* c) {
   if (c->h_dups) (void)hipHostFree(c->h_dups);
   fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
-  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT);
+  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_govf);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->h_stat) hipHostFree(c->h_stat);
@@ -1563,7 +1622,7 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   HIPCHK(hipMemcpyAsync(c->d_v, v, n * 4ull, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipMemcpyAsync(c->d_g, g, n * 4ull, hipMemcpyHostToDevice, c->s));
   TRY(build_occ(c, n));
-  TRY(ensure_tables(c, goals));
+  TRY(ensure_tables(c, goals, true));
   TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
   if (c->tun.coop && !eager_policy(c, 0)) TRY(ensure_coop(c, n));
   PlanArgs P = plan_args(c, n, 0, MODE_STEP, false);
@@ -1602,7 +1661,7 @@ static int decide_impl(tsw_ctx* c, const uint32_t* my_v, const uint32_t* my_g, u
   }
   for (uint32_t k = 0; k < tot; ++k)
     if (cell_id_ok(c, nb_g[k]) && cell_id_ok(c, nb_v[k])) goals.push_back(nb_g[k]);
-  TRY(ensure_tables(c, goals));
+  TRY(ensure_tables(c, goals, true));
   // device copies: inputs, outputs, pending lists (ping-pong)
   const size_t nb = std::max<uint32_t>(tot, 1u);
   std::vector<uint32_t> idx(n);
@@ -1769,6 +1828,7 @@ int tsw_dist_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16_t* out
   for (uint32_t g : gv)
     if (!cell_id_ok(c, g)) RET(TSW_EINVAL, "goal cell off-grid or blocked");
   TRY(ensure_tables(c, gv));
+  TRY(require_real_tables(c, gv));
   const size_t ncell = c->G.ncell;
   for (uint32_t i = 0; i < k; ++i) {
     const int32_t slot = c->h_goal_tab[gv[i]];
@@ -1822,6 +1882,7 @@ int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, cons
   if (newg.empty()) return TSW_OK;
   auto ingest = [&]() -> int {
     TRY(reserve_slots(c, newg.size(), slots));
+    for (uint32_t sl : slots) c->h_tab_tableless[sl] = 0;  // imported: real u16 tables
     const size_t ncell = c->G.ncell;
     for (size_t j = 0; j < newg.size(); ++j)
       HIPCHK(hipMemcpyAsync(c->d_dist + (size_t)slots[j] * c->tstride, dev_tables + (size_t)src[j] * ncell,
@@ -1848,7 +1909,7 @@ int tsw_next_hop_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* 
   std::vector<uint32_t> gv(goals, goals + k);
   for (uint32_t g : gv)
     if (!cell_id_ok(c, g)) RET(TSW_EINVAL, "goal cell off-grid or blocked");
-  TRY(ensure_tables(c, gv));
+  TRY(ensure_tables(c, gv, true));
   const size_t ncell = c->G.ncell;
   for (uint32_t i = 0; i < k; ++i) {
     const int32_t slot = c->h_goal_tab[gv[i]];
@@ -1860,7 +1921,7 @@ int tsw_next_hop_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* 
   return TSW_OK;
 }
 
-int tsw_next_hop_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* dev_out) {
+int tsw_next_hop_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* dev_out, uint16_t* dev_dist) {
   if (!c) return TSW_EINVAL;
   if (k == 0) return TSW_OK;
   if (!goals || !dev_out) RET(TSW_EINVAL, "null argument");
@@ -1870,6 +1931,7 @@ int tsw_next_hop_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, ui
     if (!cell_id_ok(c, g)) RET(TSW_EINVAL, "goal cell off-grid or blocked");
   HIPCHK(hipDeviceSynchronize());  // dev_out may come from another stream of the caller
   TRY(ensure_tables(c, gv));
+  TRY(require_real_tables(c, gv));
   // eager resolution of this shard's multi-candidate cells, whatever the context's policy
   std::vector<uint32_t> ug, us;
   std::vector<uint8_t> seen(c->tab_count, 0);
@@ -1887,6 +1949,11 @@ int tsw_next_hop_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, ui
     const int32_t slot = c->h_goal_tab[gv[i]];
     HIPCHK(hipMemcpyAsync(dev_out + (size_t)i * ncell, c->d_nh + (size_t)slot * c->tstride, ncell,
                           hipMemcpyDeviceToDevice, c->s));
+    // the K1 tables the codes were resolved from, out of the store (one K1 build serves both
+    // all-gathers of a shard: ADVICE r2)
+    if (dev_dist)
+      HIPCHK(hipMemcpyAsync(dev_dist + (size_t)i * ncell, c->d_dist + (size_t)slot * c->tstride, ncell * 2,
+                            hipMemcpyDeviceToDevice, c->s));
   }
   HIPCHK(hipStreamSynchronize(c->s));
   resolve_timing(c);
@@ -1907,6 +1974,7 @@ int tsw_import_next_hops_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, c
   if (newg.empty()) return TSW_OK;
   auto ingest = [&]() -> int {
     TRY(reserve_slots(c, newg.size(), slots));
+    for (uint32_t sl : slots) c->h_tab_tableless[sl] = 0;  // imported: real u16 tables
     const size_t ncell = c->G.ncell;
     for (size_t j = 0; j < newg.size(); ++j) {
       HIPCHK(hipMemcpyAsync(c->d_dist + (size_t)slots[j] * c->tstride, dev_dist + (size_t)src[j] * ncell,

@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(1024) k_bfs(DevGrid G, const uint32_t* __restr
                                               const uint32_t* __restrict__ slots, uint32_t k,
                                               uint16_t* __restrict__ dist_base, uint64_t dstride,
                                               uint8_t* __restrict__ nh_base, uint64_t nstride,
-                                              uint32_t* __restrict__ err) {
+                                              uint32_t* __restrict__ err, uint8_t* __restrict__ govf) {
   extern __shared__ __align__(16) uint32_t smem[];
   const uint32_t W = G.W, H = G.H, Ww = G.Ww, nw = H * Ww, nwp = (nw + 3u) & ~3u;
   const uint32_t ncell = G.ncell, ncp = (ncell + 7u) & ~7u;
@@ -120,6 +120,7 @@ __global__ void __launch_bounds__(1024) k_bfs(DevGrid G, const uint32_t* __restr
       ++level;
       if (level >= 0xFFFEu) {
         if (tid == 0) atomicOr(err, ERR_DIST_OVERFLOW);
+        if (tid == 0 && govf) govf[gi] = 1u;  // planned without a table (K3)
         break;
       }
       uint32_t* tmp = cur;
@@ -524,7 +525,7 @@ size_t bfs_lds_bytes(const DevGrid& G, bool lds_table) {
 
 hipError_t launch_bfs(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                       uint16_t* dist_base, uint64_t dstride, uint8_t* nh_base, uint64_t nstride,
-                      uint32_t* err, int max_lds, int num_cu, hipStream_t s) {
+                      uint32_t* err, int max_lds, int num_cu, hipStream_t s, uint8_t* govf) {
   if (k == 0) return hipSuccess;
   size_t lds_tab = bfs_lds_bytes(G, true);
   size_t lds_no = bfs_lds_bytes(G, false);
@@ -543,11 +544,11 @@ hipError_t launch_bfs(const DevGrid& G, const uint32_t* goals, const uint32_t* s
   if (use_tab) {
     hipFuncSetAttribute((const void*)k_bfs<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k_bfs<true>, dim3(grid), dim3(bd), lds, s, G, goals, slots, k, dist_base, dstride,
-                       nh_base, nstride, err);
+                       nh_base, nstride, err, govf);
   } else {
     hipFuncSetAttribute((const void*)k_bfs<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k_bfs<false>, dim3(grid), dim3(bd), lds, s, G, goals, slots, k, dist_base, dstride,
-                       nh_base, nstride, err);
+                       nh_base, nstride, err, govf);
   }
   return hipGetLastError();
 }

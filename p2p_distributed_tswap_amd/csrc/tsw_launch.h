@@ -13,7 +13,7 @@ size_t bfs_lds_bytes(const DevGrid& G, bool lds_table);
 
 hipError_t launch_bfs(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                       uint16_t* dist_base, uint64_t dstride, uint8_t* nh_base, uint64_t nstride,
-                      uint32_t* err, int max_lds, int num_cu, hipStream_t s);
+                      uint32_t* err, int max_lds, int num_cu, hipStream_t s, uint8_t* govf = nullptr);
 
 // K1 v2 (tsw_bfs.hip): one wavefront per goal. Padded layout: word (r, c) of the W x H grid
 // sits at p = (r + 1) * Wp + c, Wp = Ww + 1 (zero guard word per row, zero guard rows).
@@ -29,6 +29,7 @@ struct WaveBfsArgs {
   uint16_t* lovf;         // per-wave list overflow, 2 * npw u16 each
   uint32_t* work;         // goal dequeue counter (zeroed before the launch)
   uint32_t* err;
+  uint8_t* govf;          // optional: govf[goal index] = 1 when its distances overflow u16
   uint32_t vec16;         // 16-B stores allowed (W % 8 == 0, 16-B aligned tables)
   uint32_t max_waves;     // waves per workgroup cap
   uint64_t scratch_waves; // waves the scratch buffers are sized for
@@ -55,6 +56,7 @@ struct BlkBfsArgs {
   unsigned long long* wlg;  // per-wave west-step blocks, nbp u64 each
   uint32_t* work;         // goal dequeue counter (zeroed before the launch)
   uint32_t* err;
+  uint8_t* govf;          // optional: govf[goal index] = 1 when its distances overflow u16
   uint32_t vec16;         // 16-B stores allowed (W % 8 == 0, 16-B aligned tables)
   uint32_t stage;         // tables 16-B aligned (dist, dstride % 8 == 0): decoded rows leave through an
                           // LDS staging pass as coalesced 16-B stores (any W)
@@ -86,6 +88,7 @@ struct BigBfsArgs {
   uint64_t* wlg;          // per-workgroup west-step blocks, nbp u64 each
   uint32_t* work;         // goal dequeue counter (zeroed before the launch)
   uint32_t* err;
+  uint8_t* govf;          // optional: govf[goal index] = 1 when its distances overflow u16
   uint32_t vec16;
   uint32_t scratch_wgs;   // workgroups the scratch buffers are sized for
 };

@@ -63,11 +63,12 @@ def build_and_allgather(goals: np.ndarray, ncell: int, rank: int, world: int,
 
 
 def build_and_allgather_codes(goals: np.ndarray, ncell: int, rank: int, world: int,
-                              build_dist: Callable[[np.ndarray, "torch.Tensor"], None],
-                              build_codes: Callable[[np.ndarray, "torch.Tensor"], None], dist, device):
-    """K1 + K3 shards of this rank (`build_codes(shard_goals, out[k, ncell] uint8)` resolves every
-    next hop of its goals), then one all-gather of each. Returns (tables int16, codes uint8), both
-    [world*per, ncell] in rank-major blocks (gathered_blocks gives the goal order)."""
+                              build: Callable[[np.ndarray, "torch.Tensor", "torch.Tensor"], None], dist, device):
+    """K1 + K3 shards of this rank — `build(shard_goals, out_codes[k, ncell] uint8, out_tables[k, ncell]
+    int16)` resolves every next hop of its goals and writes the K1 tables it used (one K1 build,
+    Planner.next_hop_tables_device with dist_ptr) — then one all-gather of each. Returns (tables
+    int16, codes uint8), both [world*per, ncell] in rank-major blocks (gathered_blocks gives the
+    goal order)."""
     import torch
 
     per = shard_rows(goals.size, world)
@@ -76,8 +77,7 @@ def build_and_allgather_codes(goals: np.ndarray, ncell: int, rank: int, world: i
     local_c = torch.full((per, ncell), 0xFF, dtype=torch.uint8, device=device)
     _ready(local_d, device)
     if mine.size:
-        build_dist(mine, local_d[: mine.size])
-        build_codes(mine, local_c[: mine.size])
+        build(mine, local_c[: mine.size], local_d[: mine.size])
     full_d = torch.empty((world * per, ncell), dtype=torch.int16, device=device)
     full_c = torch.empty((world * per, ncell), dtype=torch.uint8, device=device)
     dist.all_gather_into_tensor(full_d.view(torch.uint8), local_d.view(torch.uint8))

@@ -11,7 +11,7 @@
 #   plan         bench.py planning leg only (3 plans)                  -> gpurun_out/plan.json
 #   scale:NAME   scripts/scale_bench.py NAME (c3 | wh10k | c5), full horizon -> gpurun_out/scale_NAME.jsonl
 #   scaleT:NAME:T  same, horizon capped at T timesteps
-#   profile      scripts/profile_round.sh r2 (trace + PMC per workload)
+#   profile      scripts/profile_round.sh r3 (trace + PMC per workload)
 #   astar        scripts/astar_bench.py                                -> gpurun_out/astar_bench.json
 #   bfs          scripts/bfs_bench.py (K1 cells/s, den520d + 1024^2) -> gpurun_out/bfs_bench.log
 #   rehearse2    bench.py at N=2 on one GPU over gloo                  -> gpurun_out/rehearse2.json
@@ -28,9 +28,9 @@ for step in "$@"; do
   echo "[gpu_run] $step $(date +%T)"
   case $step in
     tests|tests:*)
-      k=""; [ "$step" != tests ] && k="-k ${step#tests:}"
+      k=(); [ "$step" != tests ] && k=(-k "${step#tests:}")
       log=gpurun_out/gpu_tests.log; [ "$step" != tests ] && log=gpurun_out/gpu_tests_k.log
-      run 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread $k > $log 2>&1
+      run 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "${k[@]}" > $log 2>&1
       rc=$?; tail -3 $log; [ $rc -le 1 ] || exit $rc ;;
     smoke) run 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $? ;;
     bench) run 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $? ;;
@@ -38,7 +38,7 @@ for step in "$@"; do
     scale:*) n=${step#scale:}; run 1100 python -u scripts/scale_bench.py $n > gpurun_out/scale_$n.jsonl 2> gpurun_out/scale_$n.log || exit $? ;;
     scaleT:*) a=${step#scaleT:}; n=${a%%:*}; t=${a#*:}
       run 900 python -u scripts/scale_bench.py $n --max-t $t > gpurun_out/scale_${n}_t$t.jsonl 2> gpurun_out/scale_${n}_t$t.log || exit $? ;;
-    profile) bash scripts/profile_round.sh r2 || exit $? ;;
+    profile) bash scripts/profile_round.sh r3 || exit $? ;;
     astar) run 300 python scripts/astar_bench.py --out gpurun_out/astar_bench.json > gpurun_out/astar_bench.log 2>&1 || exit $? ;;
     bfs) run 300 python scripts/bfs_bench.py 10000 5 cave > gpurun_out/bfs_bench.log 2>&1 &&
          run 300 python scripts/bfs_bench.py 2048 3 sort >> gpurun_out/bfs_bench.log 2>&1 || exit $? ;;

@@ -8,7 +8,7 @@
 # Then: python scripts/summarize_profile.py $OUT profiles/<tag>
 # Each GPU step has its own time limit; steps are chained with && so a failure stops the run.
 set -o pipefail
-TAG=${1:-r2}
+TAG=${1:-r3}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp

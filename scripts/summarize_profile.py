@@ -16,6 +16,13 @@ lists as uncalibrated); write bytes = WRITE_SIZE * 1024.
 Writes profiles/<tag>/pmc.json, read by bench.py (profiled_traffic) only when the workload and
 its algorithmic bytes per launch match the live run.
 
+A class's PMC traffic is REFUSED (no hbm_bytes_per_launch, a "refused" reason instead) when the
+counter pass dispatched that class a different number of times than the kernel-trace pass: the
+counter run then executed a different schedule (a plan that fell back to exit mode under
+the serialising counter passes ran 212 k_plan dispatches against the trace's 1), and its bytes are
+not the timed kernel's. A stderr line from the library's watchdog in a counter pass refuses the
+whole workload for the same reason.
+
 Usage: python scripts/summarize_profile.py gpurun_out/prof_r2 profiles/r2
 """
 from __future__ import annotations
@@ -87,19 +94,33 @@ def main(src: str, dst: str):
             if not os.path.exists(p):
                 continue
             tot = collections.defaultdict(float)
+            disp = collections.defaultdict(set)
             for r in csv.DictReader(open(p)):
                 if r["Counter_Name"] == counter:
                     c = kclass(r["Kernel_Name"])
                     if c:
                         tot[c] += float(r["Counter_Value"])
+                        disp[c].add(r.get("Dispatch_Id") or r.get("Correlation_Id") or len(disp[c]))
             for c, v in tot.items():
                 cls[c][counter + "_KB_total"] = v
+                cls[c][counter + "_dispatches"] = len(disp[c])
+            err = os.path.join(src, f"{wl}_{tag}.err")
+            if os.path.exists(err) and "watchdog" in open(err, errors="replace").read():
+                for c in cls:
+                    cls[c]["refused"] = f"{counter} pass: the library's watchdog fired (another schedule than the trace)"
         res = {}
         for c, d in cls.items():
             L = max(int(launches.get(c, 0)), 1)
             e = {"launches": L, "dispatches": d["dispatches"], "device_us_per_launch": d["device_ns"] / L / 1e3,
                  "kernels": d["kernels"], "algorithmic_bytes_per_launch": algo.get(c)}
-            if "FETCH_SIZE_KB_total" in d and "WRITE_SIZE_KB_total" in d:
+            for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+                nd = d.get(counter + "_dispatches")
+                if nd is not None and nd != d["dispatches"] and "refused" not in d:
+                    d["refused"] = (f"{counter} pass ran {nd} dispatches of this class, the kernel trace "
+                                    f"{d['dispatches']}: not the traced schedule")
+            if "refused" in d:
+                e["refused"] = d["refused"]
+            elif "FETCH_SIZE_KB_total" in d and "WRITE_SIZE_KB_total" in d:
                 e["read_bytes_per_launch"] = 2 * d["FETCH_SIZE_KB_total"] * 1024 / L
                 e["write_bytes_per_launch"] = d["WRITE_SIZE_KB_total"] * 1024 / L
                 e["hbm_bytes_per_launch"] = e["read_bytes_per_launch"] + e["write_bytes_per_launch"]

@@ -32,9 +32,11 @@ def _gathered(rows, goals, world, codes):
     cbuf = _DevBuf(world * per * ncell) if codes else None
     for r, gl, off in sharding.gathered_blocks(goals, world):
         with Planner(rows) as p:
-            p.dist_tables_device(gl, dbuf.ptr.value + off * ncell * 2)
-            if codes:
-                p.next_hop_tables_device(gl, cbuf.ptr.value + off * ncell)
+            if codes:  # codes + the K1 tables they came from, one K1 build
+                p.next_hop_tables_device(gl, cbuf.ptr.value + off * ncell, dbuf.ptr.value + off * ncell * 2)
+                assert p.stats()["bfs_goals"] == gl.size
+            else:
+                p.dist_tables_device(gl, dbuf.ptr.value + off * ncell * 2)
     return dbuf, cbuf, per
 
 

@@ -89,3 +89,37 @@ def test_k1_distance_overflow_leaves_context_clean():
         for k, g in enumerate(room):
             assert np.array_equal(got[k], og.bfs(int(g)))
         assert p.stats()["tables"] == 2
+
+
+def test_overflow_goal_plans_without_table():
+    """a goal more than 65,534 steps from part of its component has no u16 table, but
+    the planning entry points still plan toward it exactly — the goal is held table-less and every
+    next hop comes from the exact A* (20-bit g; get_path uses usize g-scores, tswap.rs:288-390).
+    tsw_step and tsw_plan_mapd on the serpentine map, bit-exact vs the oracle."""
+    rows = _serpentine_plus_room()
+    cells = maps.rows_to_array(rows)
+    og = OracleGraph(cells)
+    W = 512
+    # tsw_step: two agents deep in the serpentine heading to its entry (goal 0: eccentricity > 65534),
+    # one in the room heading there too (unreachable: greedy fallback), three with room goals
+    v = np.array([200 * W + 100, 120 * W + 400, 470 * W + 10, 450 * W + 5, 460 * W + 200, 500 * W + 300],
+                 dtype=np.uint32)
+    g = np.array([0, 0, 0, 480 * W + 7, 500 * W + 300, 450 * W + 6], dtype=np.uint32)
+    with Planner(rows) as p:
+        for tick in range(5):
+            rv, rg = og.step(v, g)
+            hv, hg = p.step(v, g)
+            assert np.array_equal(hv, rv) and np.array_equal(hg, rg), f"tick {tick}"
+            v, g = rv, rg
+        assert p.stats()["tableless_goals"] >= 1
+        with pytest.raises(TswapError) as ei:  # the table-returning entry point still refuses it
+            p.dist_tables(np.array([0], dtype=np.uint32))
+        assert ei.value.code == TSW_EOVERFLOW
+    # a short MAPD plan on the serpentine (its largest component): goals far apart along the corridor
+    starts, tasks = maps.make_instance(rows, 8, 16, 0x5E4)
+    ref, rgoal = og.mapd(starts, tasks, 6, trace_goals=True)
+    with Planner(rows) as p:
+        rec, goal = p.plan_mapd_arrays(starts, tasks, 6, trace_goals=True)
+        st = p.stats()
+    assert np.array_equal(goal, rgoal) and np.array_equal(rec, ref)
+    assert st["tableless_goals"] >= 1

@@ -68,14 +68,11 @@ def _worker_codes(rank, world, port, q):
     free = np.flatnonzero(cells.reshape(-1) != ord("@")).astype(np.uint32)
     goals = free[::5]
 
-    def build_dist(g, out):
-        out.copy_(torch.from_numpy(np.stack([og.bfs(int(x)) for x in g]).view(np.int16)))
+    def build(g, out_codes, out_tables):  # one builder for both (Planner.next_hop_tables_device + dist_ptr)
+        out_codes.copy_(torch.from_numpy(np.stack([og.next_codes(int(x)) for x in g])))
+        out_tables.copy_(torch.from_numpy(np.stack([og.bfs(int(x)) for x in g]).view(np.int16)))
 
-    def build_codes(g, out):
-        out.copy_(torch.from_numpy(np.stack([og.next_codes(int(x)) for x in g])))
-
-    full_d, full_c = sharding.build_and_allgather_codes(goals, cells.size, rank, world, build_dist, build_codes,
-                                                        dist, "cpu")
+    full_d, full_c = sharding.build_and_allgather_codes(goals, cells.size, rank, world, build, dist, "cpu")
     ok = True
     for r, gl, off in sharding.gathered_blocks(goals, world):
         for j, gg in enumerate(gl):
