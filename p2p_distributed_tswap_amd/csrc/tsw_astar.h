@@ -438,14 +438,17 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     ++pops;
     const uint64_t e = wpop(Hp, len, lane);
     tick(c_pop);
-    const uint32_t cx = (uint32_t)(e >> 16) & 0xFFFFu, cy = (uint32_t)e & 0xFFFFu;
+    // entry low dword: x << 16 | label << 12 | y (y < 2^11): the popped node's label travels in its
+    // entry — a node's first pop is its lowest-g entry, i.e. its latest (strictly improving)
+    // relaxation, whose label is the one its g-score word holds — so no g-score read is needed
+    const uint32_t cx = (uint32_t)(e >> 16) & 0xFFFFu, cy = (uint32_t)e & 0x7FFu;
+    const uint32_t labc = ((uint32_t)e >> 12) & 3u;
     const uint32_t cg = hk(e) & 0x7FFFu;
     const uint32_t c = cy * W + cx;
     if (c == goal) {
       flush();
       *len_out = (int32_t)cg + 1;
-      if constexpr (GSM == 2) return (uint8_t)((GB[goal] >> 5) & 3u);
-      else return (uint8_t)((GS[goal] >> 20) & 3u);
+      return (uint8_t)labc;
     }
     // neighbour of lane dd (unsigned wrap: x - 1 at x = 0 fails the bound test); every lane
     // reads (out-of-grid lanes re-read the popped cell), the LDS reads issue together
@@ -455,14 +458,9 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     const uint32_t fx = inb ? nx : cx, fy = inb ? ny : cy;
     const uint32_t nc = fy * W + fx;
     const uint32_t fw = FB[fy * Ww + (fx >> 5)];
-    uint32_t old, labc;
-    if constexpr (GSM == 2) {
-      old = GB[nc];
-      labc = (GB[c] >> 5) & 3u;
-    } else {
-      old = GS[nc];
-      labc = (GS[c] >> 20) & 3u;
-    }
+    uint32_t old;
+    if constexpr (GSM == 2) old = GB[nc];
+    else old = GS[nc];
     const uint32_t tg = cg + 1u;
     uint32_t oldg, man = 0;
     if constexpr (GSM == 2) {
@@ -486,7 +484,7 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       } else {
         if (!ovf) GS[nc] = tagw | (lab << 20) | tg;
       }
-      ent = ((uint64_t)((f << 15) | tg) << 32) | (fx << 16) | fy;
+      ent = ((uint64_t)((f << 15) | tg) << 32) | (fx << 16) | (lab << 12) | fy;
     }
     uint64_t M = ballot64(imp);
     tick(c_nb);

@@ -25,8 +25,7 @@ import numpy as np  # noqa: E402
 from p2p_distributed_tswap_amd import Planner, maps  # noqa: E402
 
 def _wh10k():
-    rows = maps.warehouse_map(510, 220, 0x510220)
-    return (rows, *maps.make_instance(rows, 10000, 30000, 0x510220))
+    return maps.wh10k_instance()
 
 
 # name: (instance factory -> (rows, starts, tasks), CPU prefix timesteps)
@@ -40,7 +39,7 @@ INSTANCES = {
 def _heartbeat(stop, t0):
     """A long plan is one blocking C call: print progress (stderr) so a batch runner sees it is alive."""
     while not stop.wait(20.0):
-        print(f"[scale_bench] still planning, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+        print(f"[scale_bench] still running, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
 
 
 def main():
@@ -50,6 +49,10 @@ def main():
     ap.add_argument("instances", nargs="*", default=["c3", "wh10k"])
     ap.add_argument("--cpu-steps", type=int, default=0, help="CPU prefix timesteps (0: per-instance default)")
     ap.add_argument("--max-t", type=int, default=2000)
+    ap.add_argument("--diag", action="store_true", help="diagnostic library (TSW_* knobs)")
+    ap.add_argument("--cpu-windows", default="",
+                    help="comma-separated extra CPU prefixes (e.g. 20): each timed separately, so the rate of "
+                         "every window between consecutive prefixes is reported (prefix-rate spread)")
     args = ap.parse_args()
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from oracle import OracleGraph  # CPU baseline + prefix check only
@@ -64,7 +67,7 @@ def main():
         hb = threading.Thread(target=_heartbeat, args=(stop, time.perf_counter()), daemon=True)
         hb.start()
         try:
-            with Planner(rows) as p:
+            with Planner(rows, diag=args.diag) as p:
                 print(f"[scale_bench] {name}: warm-up", file=sys.stderr, flush=True)
                 p.plan_mapd_arrays(starts[:8], tasks[:8], 4)  # context warm-up (not timed)
                 p.clear_tables()
@@ -78,10 +81,28 @@ def main():
             stop.set()
         T = rec.shape[1]
         og = OracleGraph(maps.rows_to_array(rows))
+        stop = threading.Event()  # the oracle is one long C call: keep printing (batch runners see it alive)
+        hb = threading.Thread(target=_heartbeat, args=(stop, time.perf_counter()), daemon=True)
+        hb.start()
+        windows = []
+        prev_T, prev_s = 0, 0.0
+        for pre in sorted({int(x) for x in args.cpu_windows.split(",") if x}):
+            if pre >= cpu_steps:
+                continue
+            tw = time.perf_counter()
+            wrec, _ = og.mapd(starts, tasks, pre)
+            ws = time.perf_counter() - tw
+            windows.append({"timesteps": [prev_T, int(wrec.shape[1])], "s": round(ws - prev_s, 3),
+                            "agent_steps_per_s": round(n * (wrec.shape[1] - prev_T) / max(ws - prev_s, 1e-9), 1)})
+            prev_T, prev_s = int(wrec.shape[1]), ws
         tc = time.perf_counter()
         crec, _ = og.mapd(starts, tasks, cpu_steps)
         cpu_s = time.perf_counter() - tc
         ct = crec.shape[1]
+        if windows:
+            windows.append({"timesteps": [prev_T, int(ct)], "s": round(cpu_s - prev_s, 3),
+                            "agent_steps_per_s": round(n * (ct - prev_T) / max(cpu_s - prev_s, 1e-9), 1)})
+        stop.set()
         prefix_ok = bool(np.array_equal(crec, rec[:, :ct]))
         cpu_rate = n * ct / cpu_s
         out = {
@@ -92,6 +113,7 @@ def main():
             "cpu_end_to_end_s_extrapolated": round(n * T / cpu_rate, 1),
             "speedup_end_to_end": round((n * T / cpu_rate) / gpu_s, 1),
             "prefix_bit_exact": prefix_ok,
+            "cpu_prefix_windows": windows,
             "tables": st["tables"], "bfs_ms": round(st["bfs_ms"], 2), "astar_ms": round(st["astar_ms"], 2),
             "plan_ms": round(st["plan_ms"], 2), "astar_queries": st["astar_queries"],
             "astar_launches": st["astar_launches"], "plan_launches": st["walker_launches"],
