@@ -372,7 +372,11 @@ __device__ __forceinline__ WinLane win_lane(uint32_t lane) {
 // lane-parallel (each lane tests its own ancestors' choices against WinLane masks; the deepest lane
 // on the path gives the window's end) instead of a 5-step SALU walk: same path, fewer instructions
 // on the pop's dependent chain.
-__device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t lane, const WinLane& wl) {
+// `at_top(top)` runs as soon as the popped entry is known (after the first window read), so the
+// caller can issue the popped node's neighbour loads while the sift still runs.
+template <class AtTop>
+__device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t lane, const WinLane& wl,
+                                         AtTop&& at_top) {
   constexpr uint64_t M62 = (1ull << 62) - 1ull, EVEN = 0x5555555555555555ull;
   const uint32_t end = --len;
   uint32_t pos = 0;
@@ -387,7 +391,11 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
     if (first) {
       last = rl64(val, 62);
       top = rl64(val, 63);
-      if (end == 0) return last;
+      if (end == 0) {
+        at_top(last);
+        return last;
+      }
+      at_top(top);
     }
     const uint32_t key = hk(val);
     const uint32_t sib = (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
@@ -463,31 +471,37 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
   const WinLane wl = win_lane(lane);
   while (len > 0) {
     ++pops;
-    const uint64_t e = wpop(Hp, len, lane, wl);
-    tick(c_pop);
     // entry low dword: x << 16 | label << 12 | y (y < 2^11): the popped node's label travels in its
     // entry — a node's first pop is its lowest-g entry, i.e. its latest (strictly improving)
-    // relaxation, whose label is the one its g-score word holds — so no g-score read is needed
-    const uint32_t cx = (uint32_t)(e >> 16) & 0xFFFFu, cy = (uint32_t)e & 0x7FFu;
+    // relaxation, whose label is the one its g-score word holds — so no g-score read is needed.
+    // The neighbour loads are issued from inside the pop, right after its first window read (the
+    // g-score / bitmap regions are disjoint from the heap, so the sift's LDS traffic cannot alias).
+    uint32_t cx = 0, cy = 0, c = 0, fx = 0, fy = 0, nc = 0, fw = 0, old = 0;
+    bool inb = false;
+    const uint64_t e = wpop(Hp, len, lane, wl, [&](uint64_t t) {
+      cx = (uint32_t)(t >> 16) & 0xFFFFu;
+      cy = (uint32_t)t & 0x7FFu;
+      c = cy * W + cx;
+      // neighbour of lane dd (unsigned wrap: x - 1 at x = 0 fails the bound test); every lane
+      // reads (out-of-grid lanes re-read the popped cell), the LDS reads issue together
+      const uint32_t nx = cx + ddx, ny = cy + ddy;
+      inb = lane < 4u && nx < W && ny < H;
+      fx = inb ? nx : cx;
+      fy = inb ? ny : cy;
+      // cell and bitmap-word indices from the popped cell's (scalar) ones: no per-lane multiply
+      nc = c + (inb ? dcell : 0u);
+      fw = FB[cy * Ww + (inb ? drow : 0u) + (fx >> 5)];
+      if constexpr (GSM == 2) old = GB[nc];
+      else old = GS[nc];
+    });
+    tick(c_pop);
     const uint32_t labc = ((uint32_t)e >> 12) & 3u;
     const uint32_t cg = hk(e) & 0x7FFFu;
-    const uint32_t c = cy * W + cx;
     if (c == goal) {
       flush();
       *len_out = (int32_t)cg + 1;
       return (uint8_t)labc;
     }
-    // neighbour of lane dd (unsigned wrap: x - 1 at x = 0 fails the bound test); every lane
-    // reads (out-of-grid lanes re-read the popped cell), the LDS reads issue together
-    const uint32_t nx = cx + ddx, ny = cy + ddy;
-    const bool inb = lane < 4u && nx < W && ny < H;
-    const uint32_t fx = inb ? nx : cx, fy = inb ? ny : cy;
-    // cell and bitmap-word indices from the popped cell's (scalar) ones: no per-lane multiply
-    const uint32_t nc = c + (inb ? dcell : 0u);
-    const uint32_t fw = FB[cy * Ww + (inb ? drow : 0u) + (fx >> 5)];
-    uint32_t old;
-    if constexpr (GSM == 2) old = GB[nc];
-    else old = GS[nc];
     const uint32_t tg = cg + 1u;
     uint32_t oldg, man = 0;
     if constexpr (GSM == 2) {
