@@ -418,13 +418,81 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
   return top;
 }
 
+// Detour bytes of a goal's K1 table for astar_wave_par<*, *, 1>: DT[c] = (D[c] - |c - goal|_1) / 2
+// (D and the Manhattan distance share parity on a 4-grid), 255 when that is >= 255 or c is blocked /
+// unreachable. One wave; D is the slot's u16 table (16-B aligned, >= round8(ncell) entries), DT holds
+// round8(ncell) bytes. Lane l converts cells 8l .. 8l+7 of each 512-cell chunk, four chunks per round
+// with their loads issued together (the table comes from HBM: one latency per round, not per chunk).
+__device__ __forceinline__ void stage_detour(uint8_t* DT, const uint16_t* D, uint32_t ncell, uint32_t W,
+                                             uint32_t goal, uint32_t lane) {
+  const uint32_t gy = goal / W, gx = goal - gy * W;
+  const uint32_t n8 = (ncell + 7u) >> 3;
+  // (x, y) of this lane's first cell; each further chunk is 512 cells on
+  uint32_t y = (8u * lane) / W, x = 8u * lane - y * W;
+  const uint32_t sy = 512u / W, sx = 512u - sy * W;
+  const uint4* D4 = reinterpret_cast<const uint4*>(D);
+  for (uint32_t i0 = lane; i0 < n8; i0 += 256u) {
+    uint4 d4[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + 64u * u;
+      d4[u] = i < n8 ? D4[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + 64u * u;
+      const uint32_t dw[4] = {d4[u].x, d4[u].y, d4[u].z, d4[u].w};
+      uint32_t out[2] = {0u, 0u};
+      uint32_t cx = x, cy = y;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t d = (dw[k >> 1] >> (16u * (k & 1u))) & 0xFFFFu;
+        const uint32_t man = (cx > gx ? cx - gx : gx - cx) + (cy > gy ? cy - gy : gy - cy);
+        const uint32_t det = d == 0xFFFFu || d < man ? 255u : min((d - man) >> 1, 255u);
+        out[k >> 2] |= det << (8u * (k & 3u));
+        if (++cx == W) {
+          cx = 0;
+          ++cy;
+        }
+      }
+      if (i < n8) reinterpret_cast<uint2*>(DT)[i] = make_uint2(out[0], out[1]);
+      // next chunk of this lane: 512 cells on
+      x += sx;
+      y += sy;
+      if (x >= W) {
+        x -= W;
+        ++y;
+      }
+    }
+  }
+}
+
 // FB: the grid's free-cell row bitmap (DevGrid::freebits) staged in LDS, so relaxing a node
 // needs no global load.
 // PROF: pr[0..4] = pops, clocks in pops, in relaxations, in pushes, pushes (TSW_ASTAR_PROF)
-template <int GSM, bool PROF>
+//
+// DAG early exit (DAG = 1: the goal's detour bytes DT staged in LDS, see stage_detour; DAG = 2: the
+// goal's u16 K1 table DG read beside the g-score words; 0: off). Exact, from these facts about this
+// A* (consistent Manhattan heuristic, no closed set, keys (f, then smaller g)):
+//  * a node n is relaxed at most once with its optimal g = d_s(n) (later relaxations need a strictly
+//    smaller g), and that relaxation fixes came_from(n) — hence its label — for good;
+//  * n lies on a shortest start -> goal path with g optimal iff g + D[n] == d* (D = the goal's K1
+//    distance, d* = D[start]); every node of the final came_from chain is such a "DAG" node;
+//  * take the chain's last node m that is already relaxed at some moment: its successor on the chain
+//    is not relaxed yet, so m has not been expanded (its pop would have relaxed it optimally). So
+//    label(goal) = label(m) for some DAG node relaxed but not yet popped.
+// Hence once every DAG node relaxed-but-unpopped carries the same label — or the goal itself has been
+// relaxed with g = d* — label(goal) = path[1]'s direction is decided and the search stops there.
+// Those nodes are exactly the heap entries with g + D == d* (a stale entry has a larger g; an optimal
+// entry leaves the heap at its pop, the node's first). Every (dag_mask + 1) pops the wave scans the heap
+// (one ds_read per 64 entries plus a D gather, label ballots) after the pop's pushes: nothing is added
+// to the per-pop chain, and the stop comes at most dag_mask pops late.
+template <int GSM, bool PROF, int DAG = 0>
 __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag,
                                                   uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
-                                                  const uint32_t* FB, int32_t* len_out, unsigned long long* pr) {
+                                                  const uint32_t* FB, int32_t* len_out, unsigned long long* pr,
+                                                  const uint8_t* DT = nullptr, const uint16_t* DG = nullptr,
+                                                  uint32_t* npop = nullptr, uint32_t dag_mask = 15u) {
   const uint32_t lane = threadIdx.x & 63u;
   unsigned long long pops = 0, c_pop = 0, c_nb = 0, c_push = 0, npush = 0, tk = 0;
   auto tick = [&](unsigned long long& acc) {
@@ -435,6 +503,7 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     }
   };
   auto flush = [&]() {
+    if (npop) *npop = (uint32_t)pops;
     if constexpr (PROF) {
       pr[0] = pops;
       pr[1] = c_pop;
@@ -454,6 +523,18 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
   if (h0 >= (1u << 17)) {
     *len_out = -2;
     return NH_UNKNOWN;
+  }
+  // DAG early exit: d* and whether it applies (the start reaches the goal; with detour bytes every DAG
+  // node's detour (D - h) / 2 <= d* / 2 must fit below the saturated 255)
+  uint32_t dstar = 0xFFFFFFFFu;
+  bool ee = false;
+  if constexpr (DAG == 1) {
+    const uint32_t dv = DT[v];
+    dstar = h0 + 2u * dv;
+    ee = dv != 255u && dstar <= 508u;
+  } else if constexpr (DAG == 2) {
+    dstar = DG[v];
+    ee = dstar != 0xFFFFu;
   }
   if (lane == 0) {
     if constexpr (GSM == 2) GB[v] = 0x80u;
@@ -530,6 +611,7 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     uint64_t M = ballot64(imp);
     tick(c_nb);
     if (ballot64(ovf) != 0ull || len + (uint32_t)__popcll(M) > hcap) {
+      flush();
       *len_out = -2;
       return NH_UNKNOWN;
     }
@@ -542,6 +624,37 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       ++npush;
     }
     tick(c_push);
+    if constexpr (DAG != 0) {
+      // every (dag_mask + 1) pops: the labels of the heap's DAG entries (g + D == d*), and whether the
+      // goal is among them. Off the per-pop chain: one read per 64 entries plus a D gather.
+      if (ee && (pops & dag_mask) == 0u) {
+        uint32_t labs = 0, glab = 4u;
+        for (uint32_t j0 = 0; j0 < len; j0 += 64u) {
+          const uint32_t j = j0 + lane;
+          const uint64_t en = Hp[j < len ? j : 0u];
+          const uint32_t lo = (uint32_t)en, ex = lo >> 16, ey = lo & 0x7FFu, eg = hk(en) & 0x7FFFu;
+          const uint32_t ec = ey * W + ex;
+          bool d;
+          if constexpr (DAG == 1) {  // D = Manhattan to the goal + 2 * detour
+            const uint32_t eh = (ex > gx ? ex - gx : gx - ex) + (ey > gy ? ey - gy : gy - ey);
+            d = eg + eh + 2u * (uint32_t)DT[ec] == dstar;
+          } else {
+            d = eg + (uint32_t)DG[ec] == dstar;
+          }
+          d = d && j < len;
+          const uint32_t el = (lo >> 12) & 3u;
+          const uint64_t gm = ballot64(d && ec == goal);
+          if (gm) glab = rl32(el, (uint32_t)__builtin_ctzll(gm));
+          labs |= (ballot64(d && el == 0u) ? 1u : 0u) | (ballot64(d && el == 1u) ? 2u : 0u) |
+                  (ballot64(d && el == 2u) ? 4u : 0u) | (ballot64(d && el == 3u) ? 8u : 0u);
+        }
+        if (glab != 4u || __builtin_popcount(labs) == 1) {
+          flush();
+          *len_out = (int32_t)dstar + 1;
+          return (uint8_t)(glab != 4u ? glab : (uint32_t)__builtin_ctz(labs));
+        }
+      }
+    }
   }
   flush();
   *len_out = 2;

@@ -78,6 +78,8 @@ struct Tunables {
   bool avoid_xcc = true;          // TSW_WORKER_AVOID_XCD=0: coop workers also run on the planner's XCD
   bool chain_preempt = true;      // TSW_CHAIN_PREEMPT=0: chain workers finish a chain before serving queued pairs
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
+  bool dag_exit = true;           // TSW_DAG_EXIT=0: coop workers' A* runs to the goal's pop (no DAG early exit)
+  uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
 
   static Tunables from_env() {
     Tunables t;
@@ -116,6 +118,8 @@ struct Tunables {
     t.chain_preempt = num("TSW_CHAIN_PREEMPT", 0, 1, 1) != 0;
     t.avoid_xcc = num("TSW_WORKER_AVOID_XCD", 0, 1, 1) != 0;
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
+    t.dag_exit = num("TSW_DAG_EXIT", 0, 1, 1) != 0;
+    t.dag_mask = (uint32_t)num("TSW_DAG_MASK", 0, 0x7FFFFFFF, t.dag_mask);
 #endif
     return t;
   }
@@ -1132,7 +1136,12 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.epochs = c->d_epochs;
     W.heaps = c->d_heaps;
     W.ghcap = c->hcap;
-    const WorkerCfg wcfg = worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs);
+    const WorkerCfg wcfg = worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs, c->tun.dag_exit);
+    W.dag = wcfg.dag;
+    // the test's heap scan gathers D from LDS (detour bytes) or from the u16 table in global memory:
+    // every 16 / 64 pops (C3 worker busy -20 %, wh10k 400 steps 5.77 -> 5.42 s; profiles/r3/dag_exit_ab.txt)
+    W.dag_mask = c->tun.dag_mask ? c->tun.dag_mask : (W.dag == 1u ? 15u : 63u);
+    W.dist = c->d_dist;
     W.gs_lds = wcfg.gs_lds;
     W.stage_fb = wcfg.stage_fb;
     W.hcap = wcfg.hcap;
@@ -1144,8 +1153,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.nworkers = std::min(want, c->nslots);
     wblocks = W.wpb ? (W.nworkers + W.wpb - 1u) / W.wpb : 0u;
     if (c->tun.plan_debug)
-      fprintf(stderr, "[k_plan] workers: %u waves (%u per workgroup), g-scores %u, heap %u entries, %u B LDS each\n",
-              W.nworkers, W.wpb, wcfg.gs_lds, wcfg.hcap, W.lds_per_wave);
+      fprintf(stderr, "[k_plan] workers: %u waves (%u per workgroup), g-scores %u, heap %u entries, DAG exit %u, %u B LDS each\n",
+              W.nworkers, W.wpb, wcfg.gs_lds, wcfg.hcap, wcfg.dag, W.lds_per_wave);
     if (W.nworkers == 0 || wcfg.hcap < 4u) P.coop = 0;  // nothing fits beside the planner: exit mode
   }
   const bool coop = P.coop != 0;
@@ -1260,9 +1269,11 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                   (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
           fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u\n",
                   cc.waits ? (double)cc.dbg_depth / cc.waits : 0.0, cc.dbg_depth_max);
-          fprintf(stderr, "[k_plan] worker A* ms (queries): needed %.1f (%u) spec %.1f (%u) task chains %.1f (%u)\n",
-                  cc.wbusy[0] / (double)c->wall_khz, cc.wcount[0], cc.wbusy[1] / (double)c->wall_khz, cc.wcount[1],
-                  cc.wbusy[2] / (double)c->wall_khz, cc.wcount[2]);
+          fprintf(stderr, "[k_plan] worker A* ms (queries, pops): needed %.1f (%u, %llu) spec %.1f (%u, %llu) task chains "
+                  "%.1f (%u, %llu) | tier-2 hand-offs %llu tier-3 %llu | detour staging %.1f ms (%u)\n",
+                  cc.wbusy[0] / (double)c->wall_khz, cc.wcount[0], cc.wpops[0], cc.wbusy[1] / (double)c->wall_khz,
+                  cc.wcount[1], cc.wpops[1], cc.wbusy[2] / (double)c->wall_khz, cc.wcount[2], cc.wpops[2],
+                  cc.wpops[3] & 0xFFFFFFFFull, cc.wpops[3] >> 32, cc.wbusy[3] / (double)c->wall_khz, cc.wcount[3]);
         }
       }
       // exit mode: pairs the prefetch queued but no firing needed — resolve them so no table entry

@@ -84,6 +84,7 @@ struct CoopCtl {
   // diagnostics: worker wall-clock ticks inside A* and queries, by queue (needed, spec, chain)
   unsigned long long wbusy[4];
   uint32_t wcount[4];
+  unsigned long long wpops[4];  // ... and heap pops (all tiers)
   // diagnostics: speculative-queue backlog (published - claimed) when a planner wait starts
   unsigned long long dbg_depth;
   uint32_t dbg_depth_max, pad4[3];

@@ -704,16 +704,28 @@ hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const
 }
 
 
-WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs) {
+WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs,
+                        bool dag_exit) {
   const size_t fbb = (size_t)G.H * G.Ww * 4u;
   const uint32_t want = hcap_want ? std::min(hcap_want, WAVE_HCAP) : WAVE_HCAP;
+  // m: g-score placement; fb: free bitmap in LDS. With LDS g-scores the DAG early exit stages the
+  // goal's detour bytes in LDS too (its reads then cost what a g-score read costs) and the heap gives
+  // up entries past 1,024 for more waves per CU, up to one per SIMD (C3 queries peak below 300
+  // entries; an overflowing query is handed to the next tier); with global g-scores it reads the
+  // u16 table beside them.
   auto make = [&](uint32_t m, bool fb) {
     WorkerCfg c{};
     c.gs_lds = m;
     c.stage_fb = fb ? 1u : 0u;
+    c.dag = !dag_exit ? 0u : m != 0u ? 1u : 2u;
     const size_t gsb = m == 1u ? (size_t)G.ncell * 4u : m == 2u ? ((size_t)G.ncell + 15u) / 16u * 16u : 0u;
-    const size_t rest = gsb + (fb ? fbb : 0u);
+    const size_t dtb = c.dag == 1u ? ((size_t)G.ncell + 15u) / 16u * 16u : 0u;
+    const size_t rest = gsb + (fb ? fbb : 0u) + dtb;
     c.hcap = rest < WAVE_LDS_MAX ? (uint32_t)std::min<size_t>(want, (WAVE_LDS_MAX - rest) / 8u) : 0u;
+    if (c.dag == 1u && c.hcap > 1024u && hcap_want == 0u) {
+      const size_t pc = std::min<size_t>(4u, WAVE_LDS_MAX / (rest + 1024u * 8u));
+      if (pc >= 1u) c.hcap = (uint32_t)std::min<size_t>(c.hcap, (WAVE_LDS_MAX / pc - rest) / 8u);
+    }
     c.lds = (size_t)c.hcap * 8u + rest;
     const uint32_t per_cu = c.lds ? (uint32_t)std::min<size_t>(16u, WAVE_LDS_MAX / c.lds) : 0u;
     c.waves = (uint32_t)num_cu * per_cu;

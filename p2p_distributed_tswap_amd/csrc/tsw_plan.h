@@ -125,15 +125,22 @@ struct WorkerArgs {
   uint32_t wpb;        // worker waves per workgroup (each owns lds_per_wave bytes of the dynamic LDS)
   uint32_t lds_per_wave;
   uint32_t nworkers;   // worker waves in the dispatch (<= the global g-score / heap slots)
+  // exact DAG early exit of the A* (tsw_astar.h): 0 off, 1 the goal's detour bytes staged in this
+  // wave's LDS (after the free bitmap), 2 the goal's u16 table read from global memory
+  uint32_t dag;
+  const uint16_t* dist;  // K1 tables, nstride entries per goal slot
+  uint32_t dag_mask;     // the DAG test runs when (pops & dag_mask) == 0
 };
 // Worker placement: per-wave LDS (heap, g-scores, free bitmap) sets the waves per CU. g-scores stay
 // in LDS (fastest per pop) unless that leaves < 3 waves per CU while many agents can need queries at
 // once (n > 2000): then they move to the global slots and more waves run.
 struct WorkerCfg {
   uint32_t gs_lds, stage_fb, hcap, waves;
+  uint32_t dag;  // WorkerArgs::dag
   size_t lds;
 };
-WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs = -1);
+WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs = -1,
+                        bool dag_exit = true);
 
 // The plan dispatch: workgroup 0 runs k_plan's planner (block threads, lds bytes of dynamic LDS);
 // with W (coop mode) workgroups 1..worker_blocks run W->wpb K3 worker waves each.

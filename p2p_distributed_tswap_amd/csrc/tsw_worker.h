@@ -170,12 +170,15 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   uint8_t* GB = reinterpret_cast<uint8_t*>(wsm + hcap);      // gs_lds == 2
   const uint32_t gsb = gs_lds == 1u ? ncell * 4u : gs_lds == 2u ? (ncell + 15u) / 16u * 16u : 0u;
   const uint32_t* FB = G.freebits;
+  const uint32_t nfw = G.H * G.Ww;
   if (A.stage_fb) {
     uint32_t* fb = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wsm + hcap) + gsb);
-    const uint32_t nfw = G.H * G.Ww;
     for (uint32_t t = lane; t < nfw; t += 64u) fb[t] = G.freebits[t];
     FB = fb;
   }
+  // DAG early exit (A.dag == 1): the detour bytes of the goal last staged (dt_goal), after the bitmap
+  uint8_t* DT = reinterpret_cast<uint8_t*>(wsm + hcap) + gsb + (A.stage_fb ? (nfw * 4u + 15u) / 16u * 16u : 0u);
+  uint32_t dt_goal = 0xFFFFFFFFu;
   if (gs_lds == 1u)
     for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
   uint32_t* GSg = A.gs_all + (uint64_t)wid * ncell;
@@ -185,14 +188,30 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   if (lane == 0) __hip_atomic_fetch_add(&A.cc->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // exact A* for (v, goal): tier 1 LDS heap + LDS (or global) g-scores, tier 2 global u32
   // g-scores, tier 3 global heap (the k_astar_wave -> k_astar hand-off chain, in one wave)
-  auto resolve_exact = [&](uint32_t v, uint32_t goal) -> uint8_t {
+  uint32_t last_pops = 0;      // heap pops of the last query (tiers 1-2; diagnostics)
+  unsigned long long tiers = 0;  // queries handed to tier 2 (low half) / tier 3 (high half)
+  // tab: the goal's table slot (< 0: no table, no early exit)
+  auto resolve_exact = [&](uint32_t v, uint32_t goal, int32_t tab) -> uint8_t {
     int32_t L = 0;
     uint8_t code = NH_UNKNOWN;
+    uint32_t np = 0, npt = 0;  // heap pops (diagnostics)
+    const uint32_t dag = tab >= 0 ? A.dag : 0u;
+    const uint16_t* DGt = dag ? A.dist + (uint64_t)tab * A.nstride : nullptr;
+    if (dag == 1u && dt_goal != goal) {
+      const unsigned long long ts0 = wall_clock64();
+      stage_detour(DT, DGt, ncell, G.W, goal, lane);
+      dt_goal = goal;
+      if (lane == 0) {  // diagnostics: staging time / count
+        __hip_atomic_fetch_add(&A.cc->wbusy[3], wall_clock64() - ts0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&A.cc->wcount[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     if (gs_lds == 2u) {
       uint4* g4 = reinterpret_cast<uint4*>(GB);
       for (uint32_t c = lane; c < (ncell + 15u) / 16u; c += 64u) g4[c] = make_uint4(0u, 0u, 0u, 0u);
       wave_sync();
-      code = astar_wave_par<2, false>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr);
+      code = dag == 1u ? astar_wave_par<2, false, 1>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask)
+                       : astar_wave_par<2, false>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr, nullptr, nullptr, &np);
     } else if (gs_lds == 1u) {
       if (epl % 1023u == 0u && epl > 0u) {
         for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
@@ -200,29 +219,40 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
       wave_sync();
       const uint32_t tag = epl % 1023u + 1u;
       ++epl;
-      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr);
+      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask)
+                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr, nullptr, nullptr, &np);
     } else {
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
-      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr);
+      code = dag == 2u
+                 ? astar_wave_par<1, false, 2>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, DGt, &np, A.dag_mask)
+                 : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, nullptr, &np);
     }
-    if (L == -2 && gs_lds != 0u) {
+    npt = np;
+    if (L == -2 && gs_lds != 0u) {  // tier 2: global u32 g-scores (the staged detour bytes still apply)
+      tiers += 1ull;
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
-      code = astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr);
+      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask)
+                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, nullptr, &np);
+      npt += np;
     }
     if (L == -2) {
+      tiers += 1ull << 32;
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
       if (lane == 0) code = astar_one(G, v, goal, tag, Hg, A.ghcap, GSg, &L, &A.cc->err);
       code = (uint8_t)__builtin_amdgcn_readfirstlane(code);
     }
+    last_pops = npt;
     return code;
   };
   uint32_t cur_q = 0;  // queue of the query being resolved (0 needed, 1 spec, 2 chain)
-  auto resolve = [&](uint32_t v, uint32_t goal) -> uint8_t {
+  auto resolve = [&](uint32_t v, uint32_t goal, int32_t tab) -> uint8_t {
     const unsigned long long tr0 = wall_clock64();
-    const uint8_t code = resolve_exact(v, goal);
+    const uint8_t code = resolve_exact(v, goal, tab);
     if (lane == 0) {
       __hip_atomic_fetch_add(&A.cc->wbusy[cur_q], wall_clock64() - tr0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(&A.cc->wcount[cur_q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&A.cc->wpops[cur_q], (unsigned long long)last_pops, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
     }
     return code;
   };
@@ -255,7 +285,7 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     const int32_t tab = (int32_t)w_ld(e + 2);
     cur_q = (uint32_t)which;
     if (which < 2) {
-      publish_code(v, tab, resolve(v, goal), false);
+      publish_code(v, tab, resolve(v, goal, tab), false);
       continue;
     }
     // task chain: the path an agent carrying this task walks from its pickup to the delivery
@@ -279,12 +309,12 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
         const uint32_t v2 = w_ld(e2), g2 = w_ld(e2 + 1);
         const int32_t t2 = (int32_t)w_ld(e2 + 2);
         cur_q = (uint32_t)w2;
-        publish_code(v2, t2, resolve(v2, g2), false);
+        publish_code(v2, t2, resolve(v2, g2, t2), false);
         cur_q = 2u;
       }
       uint8_t code = (uint8_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(c, tab) : 0u);
       if (code == NH_UNKNOWN) {
-        code = resolve(c, goal);
+        code = resolve(c, goal, tab);
         publish_code(c, tab, code, true);
       }
       if (code >= NH_STAY) break;  // stay (unreachable goal), pending elsewhere, or overflow
@@ -293,6 +323,7 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   }
   if (lane == 0) {
     A.epochs[wid] = ep;
+    if (tiers) __hip_atomic_fetch_add(&A.cc->wpops[3], tiers, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every exit path after the increment: the planner's "no worker left" test reads this
     __hip_atomic_fetch_sub(&A.cc->alive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
