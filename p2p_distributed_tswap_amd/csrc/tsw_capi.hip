@@ -70,6 +70,7 @@ struct Tunables {
   uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
   uint32_t prefetch_ext = 7;      // TSW_PREFETCH_EXT: bit 0 DAG from an agent's own unresolved cell, bit 1 walk past the pickup, bit 2 walk-ahead for agents a firing changed (C3 476 -> 409 ms with bits 0-1)
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
+  uint32_t part_lds = 0x7F;       // TSW_PART_LDS: PART_* agent arrays allowed in LDS one by one (tsw_plan.h)
   bool occ_split = true;          // TSW_OCC_SPLIT=0: the occupancy grid goes to LDS only together with MU
   uint32_t plan_block = 0;        // TSW_PLAN_BLOCK: k_plan workgroup size (0 = auto)
   bool plan_debug = false;        // TSW_PLAN_DEBUG: k_plan sub-phase ticks printed per plan
@@ -110,6 +111,7 @@ struct Tunables {
     t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 16, t.dag_prefetch);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
+    t.part_lds = (uint32_t)num("TSW_PART_LDS", 0, 0x7F, t.part_lds);
     t.occ_split = num("TSW_OCC_SPLIT", 0, 1, 1) != 0;
     t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
@@ -1073,13 +1075,21 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   // LDS residency, in priority order: agents, occupancy grid, task table
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
-  // without the agent arrays, the rules relabel's pointer-doubling buffers come next
-  bool fl = !ag && c->tun.flinks_lds && plan_lds_bytes(n, P.ncell, m, false, false, false, true) <= budget;
+  // without the whole set, single agent arrays in priority order (PART_*: the rules phase's serial
+  // successor walks and firing scans read SUCC / ONC / V / G; wh10k rules 3.9 -> ? s), then the rules
+  // relabel's pointer-doubling buffers
+  uint32_t part = 0;
+  if (!ag)
+    for (uint32_t bit : {PART_SUCC, PART_ONC, PART_V, PART_G, PART_NHC, PART_CANDC, PART_GT})
+      if ((c->tun.part_lds & bit) && plan_lds_bytes(n, P.ncell, m, false, false, false, false, true, part | bit) <= budget)
+        part |= bit;
+  bool fl = !ag && c->tun.flinks_lds && plan_lds_bytes(n, P.ncell, m, false, false, false, true, true, part) <= budget;
   // the occupancy grid with the movement rounds' MU words, else OCC alone (every rules round reads
   // OCC: C3's 170x84 fits OCC but not MU beside the agent arrays)
-  bool mu = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, true) <= budget;
-  bool oc = mu || (c->tun.occ_split && plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, false) <= budget);
-  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl, mu) <= budget;
+  bool mu = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, true, part) <= budget;
+  bool oc = mu || (c->tun.occ_split && plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, false, part) <= budget);
+  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl, mu, part) <= budget;
+  P.part_lds = part;
   P.f_lds = fl;
   P.mu_lds = mu;
   P.agents_lds = ag;
@@ -1109,7 +1119,7 @@ int build_occ(tsw_ctx* c, uint32_t n) {
 int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   *c->h_ctl = init;
   HIPCHK(hipMemcpyAsync(c->d_ctl, c->h_ctl, sizeof(PlanCtl), hipMemcpyHostToDevice, c->s));
-  size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds, P.mu_lds);
+  size_t lds = plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds, P.mu_lds, P.part_lds);
   // coop mode: the planner block reserves its CU's whole LDS so no worker wave is placed beside it
   // (they would compete for its SIMDs and LDS bandwidth on the critical path)
   if (P.coop) lds = std::max<size_t>(lds, (size_t)std::max(c->max_lds - 2048, 0));
@@ -1157,6 +1167,10 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
               W.nworkers, W.wpb, wcfg.gs_lds, wcfg.hcap, wcfg.dag, W.lds_per_wave);
     if (W.nworkers == 0 || wcfg.hcap < 4u) P.coop = 0;  // nothing fits beside the planner: exit mode
   }
+  if (c->tun.plan_debug)
+    fprintf(stderr, "[k_plan] planner LDS: agents %u part 0x%x flinks %u occ %u mu %u tasks %u (%zu B)\n", P.agents_lds,
+            P.part_lds, P.f_lds, P.occ_lds, P.mu_lds, P.tasks_lds,
+            plan_lds_bytes(P.n, P.ncell, P.m, P.agents_lds, P.occ_lds, P.tasks_lds, P.f_lds, P.mu_lds, P.part_lds));
   const bool coop = P.coop != 0;
   // every return below happens after the dispatch has drained (workers included): nothing of this
   // call keeps running into the next one

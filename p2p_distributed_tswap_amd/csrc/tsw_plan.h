@@ -48,6 +48,7 @@ struct PlanArgs {
   uint32_t has_dups, prefetch;  // prefetch: enqueue rules-round next hops up front (rules_prefetch)
   uint32_t f_lds;               // F1/F2 carved in LDS although the agent arrays are global
   uint32_t mu_lds;              // occ_lds and the movement rounds' MU words in LDS too
+  uint32_t part_lds;            // !agents_lds: PART_* agent arrays carved in LDS anyway (flat accesses)
   uint32_t wave_rules_max;      // rules rounds run in wave 0 alone when n <= this
   uint32_t wide_prefetch;       // 0: off; else also (succ cell, goal) of every agent, path walked this many hops ahead
   uint32_t dag_prefetch;        // walk-ahead also queues the shortest-path successors of the first unresolved cell
@@ -94,9 +95,16 @@ struct PlanArgs {
   uint32_t* hflags;
 };
 
+// Agent arrays that go to LDS one by one when all of them do not fit (PlanArgs::part_lds), in the
+// order the host admits them: the rules phase's successor chains and labels first (its relabel walks
+// and firing scans are serial dependent loads), then cells and goals, then the code caches.
+enum : uint32_t {
+  PART_SUCC = 1u, PART_ONC = 2u, PART_V = 4u, PART_G = 8u, PART_NHC = 16u, PART_CANDC = 32u, PART_GT = 64u,
+};
+size_t part_lds_bytes(uint32_t n, uint32_t part);
 // flinks: the pointer-doubling buffers F1/F2 alone in LDS (when the agent arrays are not)
 size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks, bool flinks = false,
-                      bool mu = true);
+                      bool mu = true, uint32_t part = 0u);
 hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cnt, uint32_t ncell, uint32_t* dups,
                       hipStream_t s);
 // Coop-mode K3 workers (tsw_worker.h) run in the workgroups 1.. of the plan dispatch: claim queued

@@ -782,10 +782,18 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     S.ONC = carve(n);
     S.CANDC = carve(n);
   } else {
-    S.V = P.v;
-    S.G = P.g;
-    S.GT = P.gt;
-    S.SUCC = P.succ;
+    // arrays the host admitted to LDS (part_lds; carve order = part_lds_bytes' order), else global
+    auto pick32 = [&](uint32_t bit, uint32_t* g) {
+      return (P.part_lds & bit) ? reinterpret_cast<uint32_t*>(carve((size_t)n * 4)) : g;
+    };
+    auto pick8 = [&](uint32_t bit, uint8_t* g) { return (P.part_lds & bit) ? carve(n) : g; };
+    S.SUCC = pick32(PART_SUCC, P.succ);
+    S.V = pick32(PART_V, P.v);
+    S.G = pick32(PART_G, P.g);
+    S.GT = reinterpret_cast<int32_t*>(pick32(PART_GT, reinterpret_cast<uint32_t*>(P.gt)));
+    S.ONC = pick8(PART_ONC, P.onc);
+    S.NHC = pick8(PART_NHC, P.nhc);
+    S.CANDC = pick8(PART_CANDC, P.candc);
     if (P.f_lds) {  // pointer doubling (rules_init) on LDS instead of global memory
       S.F1 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
       S.F2 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
@@ -793,10 +801,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       S.F1 = P.f1;
       S.F2 = P.f2;
     }
-    S.NHC = P.nhc;
     S.DEC = P.dec;
-    S.ONC = P.onc;
-    S.CANDC = P.candc;
     S.MK = P.mk;  // (batched firing runs only with the agent arrays in LDS; this copy stays unused)
   }
   if constexpr (OC) {
@@ -826,6 +831,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       S.V[k] = P.v[k];
       S.G[k] = g;
       S.DEC[k] = P.dec[k];
+    } else {
+      if (P.part_lds & PART_V) S.V[k] = P.v[k];
+      if (P.part_lds & PART_G) S.G[k] = g;
     }
     S.GT[k] = P.goal_tab[g];
     S.NHC[k] = NHC_DIRTY;
@@ -1852,6 +1860,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       P.g[k] = S.G[k];
       P.dec[k] = S.DEC[k];
     }
+  else if (P.part_lds & (PART_V | PART_G))
+    for (uint32_t k = tid; k < n; k += bd) {
+      if (P.part_lds & PART_V) P.v[k] = S.V[k];
+      if (P.part_lds & PART_G) P.g[k] = S.G[k];
+    }
   if constexpr (OC)
     for (uint32_t c = tid; c < P.ncell; c += bd) P.occ[c] = S.OCC[c];
   if (tid == 0) {
@@ -1892,12 +1905,25 @@ __global__ void k_occ_flag(uint32_t* occ, const uint32_t* cnt, uint32_t ncell, u
   }
 }
 
+size_t part_lds_bytes(uint32_t n, uint32_t part) {
+  auto r16 = [](size_t b) { return (b + 15u) & ~(size_t)15u; };
+  size_t b = 0;
+  for (uint32_t bit : {PART_SUCC, PART_V, PART_G, PART_GT})
+    if (part & bit) b += r16((size_t)n * 4);
+  for (uint32_t bit : {PART_ONC, PART_NHC, PART_CANDC})
+    if (part & bit) b += r16(n);
+  return b;
+}
+
 size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool occ, bool tasks, bool flinks,
-                      bool mu) {
+                      bool mu, uint32_t part) {
   auto r16 = [](size_t b) { return (b + 15u) & ~(size_t)15u; };
   size_t b = r16(1024 * 4);
   if (agents) b += 4 * r16((size_t)n * 4) + 3 * r16((size_t)(n + 1) * 4) + 4 * r16(n);
-  else if (flinks) b += 2 * r16((size_t)(n + 1) * 4);
+  else {
+    b += part_lds_bytes(n, part);
+    if (flinks) b += 2 * r16((size_t)(n + 1) * 4);
+  }
   if (occ) b += r16((size_t)ncell * 4) + (mu ? r16((size_t)ncell * 8) : 0u);
   if (tasks) b += r16((size_t)m * 4) + r16(m);
   return b;
