@@ -707,6 +707,8 @@ hipError_t launch_bfs_blk(const BlkBfsArgs& A0, int max_lds, int num_cu, hipStre
       std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)num_cu, (A.k + gpw * nwv - 1u) / (gpw * nwv)));
   if ((uint64_t)grid * nwv * gpw > A.scratch_waves) return hipErrorInvalidValue;  // scratch per goal slot
   const size_t lds = shared + nwv * per_wave;
+#ifdef TSW_DIAG
+  // the WLS / PAIR A/B variants exist in the diagnostic build only (both measured slower)
   const void* fn = wls ? (pair ? (const void*)k_bfs_blk<true, true> : (const void*)k_bfs_blk<true, false>)
                        : (pair ? (const void*)k_bfs_blk<false, true> : (const void*)k_bfs_blk<false, false>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -715,6 +717,13 @@ hipError_t launch_bfs_blk(const BlkBfsArgs& A0, int max_lds, int num_cu, hipStre
   else if (wls) hipLaunchKernelGGL((k_bfs_blk<true, false>), dim3(grid), dim3(nwv * 64u), lds, s, A);
   else if (pair) hipLaunchKernelGGL((k_bfs_blk<false, true>), dim3(grid), dim3(nwv * 64u), lds, s, A);
   else hipLaunchKernelGGL((k_bfs_blk<false, false>), dim3(grid), dim3(nwv * 64u), lds, s, A);
+#else
+  if (wls || pair) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute((const void*)k_bfs_blk<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_bfs_blk<false, false>), dim3(grid), dim3(nwv * 64u), lds, s, A);
+#endif
   return hipGetLastError();
 }
 

@@ -465,10 +465,13 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
     } else if (!serial) {
       code = gs_lds == 2u ? astar_wave_par<2, false>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr)
                           : astar_wave_par<1, false>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr);
-    } else if (lane == 0) {
+    }
+#ifdef TSW_DIAG
+    else if (lane == 0) {  // lone-lane core (TSW_ASTAR_SERIAL A/B, diagnostic build only)
       code = gs_lds == 2u ? astar_wave_core<2>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L)
                           : astar_wave_core<1>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, &L);
     }
+#endif
     if (prof && lane == 0) {  // TSW_ASTAR_PROF: pops, shader clocks, 100 MHz ticks per query
       prof[8ull * qi + 1] = __builtin_amdgcn_s_memtime() - t0;
       prof[8ull * qi + 2] = __builtin_amdgcn_s_memrealtime() - r0;

@@ -385,3 +385,24 @@ def test_mapd_coop_workers_in_plan_dispatch():
     st = _plan_vs_oracle(rows, starts, tasks, 150)
     assert st["coop_workers"] > 0 and st["walker_launches"] == 1 and sum(st["plan_exits"]) == 0
     assert st["coop_worker_busy_ms"][0] + st["coop_worker_busy_ms"][1] > 0 and st["watchdog_fires"] == 0
+
+
+@pytest.mark.parametrize("env", [{"TSW_DAG_EXIT": "0"}, {"TSW_TASK_CHAINS": "0"}, {"TSW_DAG_MASK": "1"}])
+def test_mapd_coop_knobs(monkeypatch, env):
+    """Coop-mode A/B knobs (diagnostic build) on the C3 prefix, bit-exact: the workers' A* without the
+    DAG early exit, with the exit tested after every pop, and without task-chain jobs."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rows, starts, tasks = maps.config_instance("c3_warehouse_170x84")
+    st = _plan_vs_oracle(rows, starts, tasks, 150, diag=True)
+    assert st["coop_workers"] > 0 and st["watchdog_fires"] == 0
+
+
+@pytest.mark.parametrize("mask", [0, 0x3, 0x7F])
+def test_mapd_partial_lds_agent_arrays(monkeypatch, mask):
+    """6,000 agents: the agent arrays do not fit LDS as a set, so k_plan admits them one by one
+    (PlanArgs::part_lds, TSW_PART_LDS mask): none, SUCC + ONC, all that fit — bit-exact each way."""
+    monkeypatch.setenv("TSW_PART_LDS", str(mask))
+    rows = maps.random_map(128, 128, 0.1, 0x6000)
+    starts, tasks = maps.make_instance(rows, 6000, 600, 0x6001)
+    _plan_vs_oracle(rows, starts, tasks, 30, diag=True)
