@@ -100,6 +100,7 @@ struct PlanArgs {
 // and firing scans are serial dependent loads), then cells and goals, then the code caches.
 enum : uint32_t {
   PART_SUCC = 1u, PART_ONC = 2u, PART_V = 4u, PART_G = 8u, PART_NHC = 16u, PART_CANDC = 32u, PART_GT = 64u,
+  PART_PG = 0x3Fu,  // the subset k_plan<false, *, *, true> carves unconditionally (LDS-typed accesses)
 };
 size_t part_lds_bytes(uint32_t n, uint32_t part);
 // flinks: the pointer-doubling buffers F1/F2 alone in LDS (when the agent arrays are not)

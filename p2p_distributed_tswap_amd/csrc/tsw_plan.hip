@@ -734,7 +734,10 @@ __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
 
 // AG: every agent array in LDS. OC: the occupancy grid OCC in LDS; MUL: the movement rounds' MU
 // words too (OC alone fits grids whose MU does not, e.g. C3's 170x84 beside the agent arrays).
-template <bool AG, bool OC, bool MUL>
+// AG: every agent array in LDS. PG (!AG): the fixed subset PART_PG (SUCC, V, G, ONC, NHC, CANDC) in
+// LDS — carved unconditionally, so its accesses compile to ds_* instead of flat instructions (a flat
+// access waits for every outstanding global load as well). Otherwise part_lds picks arrays at run time.
+template <bool AG, bool OC, bool MUL, bool PG>
 __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
   extern __shared__ __align__(16) uint8_t smem[];
   if (blockIdx.x != 0) {  // coop mode: a K3 worker workgroup (tsw_worker.h), Wk.wpb single-wave workers
@@ -781,6 +784,23 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     S.DEC = carve(n);
     S.ONC = carve(n);
     S.CANDC = carve(n);
+  } else if constexpr (PG) {
+    S.SUCC = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
+    S.V = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
+    S.G = reinterpret_cast<uint32_t*>(carve((size_t)n * 4));
+    S.GT = P.gt;
+    S.ONC = carve(n);
+    S.NHC = carve(n);
+    S.CANDC = carve(n);
+    if (P.f_lds) {
+      S.F1 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
+      S.F2 = reinterpret_cast<uint32_t*>(carve((size_t)(n + 1) * 4));
+    } else {
+      S.F1 = P.f1;
+      S.F2 = P.f2;
+    }
+    S.DEC = P.dec;
+    S.MK = P.mk;
   } else {
     // arrays the host admitted to LDS (part_lds; carve order = part_lds_bytes' order), else global
     auto pick32 = [&](uint32_t bit, uint32_t* g) {
@@ -1937,13 +1957,13 @@ hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cn
   return hipGetLastError();
 }
 
-template <bool AG, bool OC, bool MUL>
+template <bool AG, bool OC, bool MUL, bool PG = false>
 static hipError_t launch_plan_t(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                                 hipStream_t s) {
-  hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC, MUL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds);
+  hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC, MUL, PG>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_plan<AG, OC, MUL>), dim3(grid), dim3(block), lds, s, P, W);
+  hipLaunchKernelGGL((k_plan<AG, OC, MUL, PG>), dim3(grid), dim3(block), lds, s, P, W);
   return hipGetLastError();
 }
 
@@ -1957,6 +1977,7 @@ hipError_t launch_plan(const PlanArgs& P, const WorkerArgs* W, uint32_t worker_b
   if (P.agents_lds && mu) return launch_plan_t<true, true, true>(P, A, grid, lds, block, s);
   if (P.agents_lds && P.occ_lds) return launch_plan_t<true, true, false>(P, A, grid, lds, block, s);
   if (P.agents_lds) return launch_plan_t<true, false, false>(P, A, grid, lds, block, s);
+  if (P.part_lds == PART_PG && !P.occ_lds) return launch_plan_t<false, false, false, true>(P, A, grid, lds, block, s);
   if (mu) return launch_plan_t<false, true, true>(P, A, grid, lds, block, s);
   if (P.occ_lds) return launch_plan_t<false, true, false>(P, A, grid, lds, block, s);
   return launch_plan_t<false, false, false>(P, A, grid, lds, block, s);

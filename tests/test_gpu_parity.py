@@ -398,7 +398,7 @@ def test_mapd_coop_knobs(monkeypatch, env):
     assert st["coop_workers"] > 0 and st["watchdog_fires"] == 0
 
 
-@pytest.mark.parametrize("mask", [0, 0x3, 0x7F])
+@pytest.mark.parametrize("mask", [0, 0x3, 0x3F, 0x7F])
 def test_mapd_partial_lds_agent_arrays(monkeypatch, mask):
     """6,000 agents: the agent arrays do not fit LDS as a set, so k_plan admits them one by one
     (PlanArgs::part_lds, TSW_PART_LDS mask): none, SUCC + ONC, all that fit — bit-exact each way."""
