@@ -1269,8 +1269,9 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
         fprintf(stderr, "[k_plan] PRE1 publish us %.0f (%llu) | rules init us %.0f prefetch us %.0f publish us %.0f (%llu)\n",
                 tk[24] / 100.0, tk[25], tk[26] / 100.0, tk[27] / 100.0, tk[28] / 100.0, tk[29]);
         fprintf(stderr, "[k_plan] wave rules kcycles: load %.0f stale %.0f fast %.0f update %.0f slow %.0f rot %.0f | "
-                "loads %llu fast firings %llu\n", tk[16] / 1e3, tk[17] / 1e3, tk[18] / 1e3, tk[19] / 1e3, tk[20] / 1e3,
-                tk[21] / 1e3, tk[22], tk[23]);
+                "loads %llu fast firings %llu | rotations %llu, settle kcycles: successors %.0f walk %.0f\n",
+                tk[16] / 1e3, tk[17] / 1e3, tk[18] / 1e3, tk[19] / 1e3, tk[20] / 1e3, tk[21] / 1e3, tk[22], tk[23],
+                tk[11], tk[30] / 1e3, tk[31] / 1e3);
         fprintf(stderr, "[k_plan] steps %u rule rounds %u move rounds %u launches %llu | move A-E us %.0f %.0f %.0f %.0f %.0f"
                 " | rules scan %.0f fire %.0f relabel %.0f\n", k.steps_run, k.rule_rounds, k.move_rounds,
                 (unsigned long long)round + 1ull, tk[8] / 100.0, tk[9] / 100.0, tk[10] / 100.0, tk[11] / 100.0,

@@ -750,6 +750,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
   }
   __shared__ PlanCtl s_ctl;
   __shared__ uint32_t s_q[5], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
+  __shared__ uint32_t s_ap[128];  // rules: members of a rule-4 cycle rotated by the wave (<= 64), links
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[32], s_tlast, s_tp;
@@ -1089,7 +1090,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         bool fs, b_at, s_at;
       };
       // FO_ROT: a rule-4 rotation of o.ns members (listed in S.F2) whose next hops are dirty
-      constexpr uint32_t FO_MISS = 1u, FO_RESCAN = 2u, FO_ROT = 4u;
+      // FO_WAVE (with FO_ROT): the wave rotated the cycle itself, members in s_ap
+      constexpr uint32_t FO_MISS = 1u, FO_RESCAN = 2u, FO_ROT = 4u, FO_WAVE = 8u;
       auto fire = [&](uint32_t b) -> FireOut {
         FireOut o;
         o.flags = 0;
@@ -1197,8 +1199,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       // relabel from the members (lane 0; the labels were exact before the rotation and only the
       // members' successors changed). False (block path: refresh, wait, relabel) if a code is
       // unresolved or a walk runs long.
-      auto rot_settle = [&](uint32_t L) -> bool {
-        const uint32_t* ap = S.F2;
+      auto rot_settle = [&](uint32_t L, const uint32_t* ap) -> bool {
         bool bad = false;
         for (uint32_t i = lane; i < L; i += 64u) {
           const uint32_t a = ap[i];
@@ -1215,11 +1216,87 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
           else bad = true;
         }
         if (__ballot(bad)) return false;
-        __threadfence_block();
-        for (uint32_t i = lane; i < L; i += 64u) relabel_reset(P, S, ap[i]);  // lanes in parallel
-        __threadfence_block();
         uint32_t ok = 0;
-        if (lane == 0) ok = relabel_walks(P, S, ap, L, 4096u) ? 1u : 0u;
+        if constexpr (AG || PG) {
+          if (L <= 64u) {
+            // Agent arrays in LDS, L <= 64: the relabel walks of all members run at once, one lane each.
+            // Only the members' successors changed, so a new cycle passes through a member, no member
+            // lies on a standing (labelled) cycle (they formed the rotated one), and a walk from a member
+            // ends at TERM / a self-loop / a labelled node (no cycle) or at a member (marked ONC = 2 + its
+            // index): the members' "next member" links then form a graph of <= 64 nodes whose cycles are
+            // exactly the new cycles; their members label them. Same labels as relabel_walks.
+            wave_order();
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the code stores above are visible
+            const unsigned long long rt0 = P.dbg ? clock64() : 0ull;
+            uint8_t cc = NHC_DIRTY;
+            uint32_t a = 0;
+            const bool mem = lane < L;
+            if (mem) {
+              a = ap[lane];
+              const uint32_t sa = succ_of(P, S, a);
+              S.SUCC[a] = sa;
+              S.ONC[a] = (uint8_t)(2u + lane);
+              const int32_t ta = S.GT[a];
+              if (sa != SUCC_TERM && sa != a && ta >= 0) cc = P.nh[(uint64_t)ta * P.nstride + S.V[sa]];
+            }
+            wave_order();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            const unsigned long long rt1 = P.dbg ? clock64() : 0ull;
+            uint32_t nm = 64u;  // next member's index (64: the walk ended without one)
+            bool fail = false;
+            if (mem) {
+              uint32_t x = S.SUCC[a];
+              for (uint32_t steps = 0; x != SUCC_TERM; ++steps) {
+                const uint32_t o = S.ONC[x], nx = S.SUCC[x];
+                if (o >= 2u) {
+                  nm = o - 2u;
+                  break;
+                }
+                if (o != 0u || nx == x) break;  // labelled standing cycle / chain end
+                if (steps >= 4096u) {
+                  fail = true;
+                  break;
+                }
+                x = nx;
+              }
+            }
+            if (mem) s_ap[64u + lane] = nm;  // (s_ap holds 128 entries: members, then next-member links)
+            wave_order();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            bool on = false;
+            if (mem) {
+              uint32_t y = nm;
+              for (uint32_t t = 0; t < L && y < 64u && !on; ++t) {
+                on = y == lane;
+                y = s_ap[64u + y];
+              }
+            }
+            wave_order();
+            if (mem && !on) S.ONC[a] = 0;
+            wave_order();
+            if (on) {  // label the cycle through a (members and the non-members between them)
+              uint32_t y = a;
+              do {
+                S.ONC[y] = 1;
+                y = S.SUCC[y];
+              } while (y != a);
+            }
+            if (mem) S.CANDC[a] = cc;
+            wave_order();
+            ok = __ballot(fail) ? 0u : 1u;
+            if (P.dbg && lane == 0) {  // diagnostics: rotation settle split (successors | walks)
+              const unsigned long long rt2 = clock64();
+              s_tick[30] += rt1 - rt0;
+              s_tick[31] += rt2 - rt1;
+            }
+          }
+        }
+        if (!(AG || PG) || L > 64u) {
+          __threadfence_block();
+          for (uint32_t i = lane; i < L; i += 64u) relabel_reset(P, S, ap[i]);  // lanes in parallel
+          __threadfence_block();
+          if (lane == 0) ok = relabel_walks(P, S, ap, L, 4096u) ? 1u : 0u;
+        }
         if (!__builtin_amdgcn_readfirstlane(ok)) return false;
         if (lane == 0) s_ctl.relabel_inc += 1;
         __threadfence_block();
@@ -1465,19 +1542,76 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                 ++rr;
                 prof(18);
               } else {
-                if (lane == 0) s_cnt = nc;
-                __threadfence_block();
-                if (lane == l) {
-                  s_best = b;
-                  s_miss = 0;
-                  const FireOut r = fire(b);
-                  r_fl = r.flags;
-                  r_s = r.s;
-                  r_ns = r.ns;
-                  r_bits = (r.fs ? 1u : 0u) | (r.b_at ? 2u : 0u) | (r.s_at ? 4u : 0u);
+                // rule 4 (tswap.rs:205-249) with the agent arrays in LDS: lane 0 lists the cycle's
+                // members (<= 64), then every member's lane rotates its goal at once — the serial
+                // rotation of fire() reads and writes the members one after another, and with the goal
+                // slots GT in global memory that was one memory latency per member
+                bool wave_rot = false;
+                if constexpr (AG || PG) {
+                  const uint32_t s4 = (uint32_t)__builtin_amdgcn_readlane((int)sk, (int)l);
+                  if (S.V[s4] != S.G[s4]) {
+                    uint32_t L = 0;
+                    if (lane == 0) {
+                      uint32_t a = b;
+                      do {
+                        if (L < 64u) s_ap[L] = a;
+                        ++L;
+                        a = S.SUCC[a];
+                      } while (a != b && L <= 64u);
+                    }
+                    L = (uint32_t)__builtin_amdgcn_readfirstlane((int)L);
+                    wave_order();
+                    if (L <= 64u) {
+                      wave_rot = true;
+                      uint32_t a = 0, ng = 0;
+                      int32_t nt = 0;
+                      if (lane < L) {  // a takes the goal of its predecessor on the cycle (last -> b)
+                        a = s_ap[lane];
+                        const uint32_t pa = s_ap[lane == 0u ? L - 1u : lane - 1u];
+                        ng = S.G[pa];
+                        nt = S.GT[pa];
+                      }
+                      wave_order();
+                      __threadfence_block();
+                      if (lane < L) {
+                        S.G[a] = ng;
+                        S.GT[a] = nt;
+                        S.NHC[a] = NHC_DIRTY;
+                      }
+                      if (nc != NO_AGENT && nc + L <= LIST_CAP) {
+                        if (lane < L) list[nc + lane] = a;
+                        nc += L;
+                      } else {
+                        nc = NO_AGENT;
+                      }
+                      if (lane == 0) {
+                        s_best = b;
+                        s_miss = 0;
+                        s_ctl.i = b + 1;
+                        s_ctl.rule_rounds += 1;
+                        if (P.dbg) s_tick[11] += 1;  // diagnostics: rule-4 rotations
+                      }
+                      r_fl = FO_ROT | FO_WAVE;
+                      r_ns = L;
+                      __threadfence_block();
+                    }
+                  }
                 }
-                __threadfence_block();
-                nc = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_cnt);
+                if (!wave_rot) {
+                  if (lane == 0) s_cnt = nc;
+                  __threadfence_block();
+                  if (lane == l) {
+                    s_best = b;
+                    s_miss = 0;
+                    const FireOut r = fire(b);
+                    r_fl = r.flags;
+                    r_s = r.s;
+                    r_ns = r.ns;
+                    r_bits = (r.fs ? 1u : 0u) | (r.b_at ? 2u : 0u) | (r.s_at ? 4u : 0u);
+                  }
+                  __threadfence_block();
+                  nc = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_cnt);
+                }
                 prof(20);
               }
               __threadfence_block();
@@ -1486,7 +1620,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               if (fl & FO_ROT) {
                 // settle the rotation inside the wave when every member's new next hop is already
                 // resolved (the rules prefetch queued them): rescan from b + 1 without a block join
-                const bool settled = rot_settle((uint32_t)__builtin_amdgcn_readlane((int)r_ns, (int)l));
+                const bool settled = rot_settle((uint32_t)__builtin_amdgcn_readlane((int)r_ns, (int)l),
+                                                 (fl & FO_WAVE) ? s_ap : S.F2);
                 prof(21);
                 if (settled) {
                   base = b + 1u;
