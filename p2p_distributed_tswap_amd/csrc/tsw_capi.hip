@@ -81,6 +81,7 @@ struct Tunables {
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
   bool dag_exit = true;           // TSW_DAG_EXIT=0: coop workers' A* runs to the goal's pop (no DAG early exit)
   uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
+  uint64_t worker_idle_us = 5000000;  // TSW_WORKER_IDLE_US: an idle coop worker exits after this long (test knob)
 
   static Tunables from_env() {
     Tunables t;
@@ -122,6 +123,7 @@ struct Tunables {
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
     t.dag_exit = num("TSW_DAG_EXIT", 0, 1, 1) != 0;
     t.dag_mask = (uint32_t)num("TSW_DAG_MASK", 0, 0x7FFFFFFF, t.dag_mask);
+    t.worker_idle_us = (uint64_t)num("TSW_WORKER_IDLE_US", 1, 5000000, (long)t.worker_idle_us);
 #endif
     return t;
   }
@@ -1151,6 +1153,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     // the test's heap scan gathers D from LDS (detour bytes) or from the u16 table in global memory:
     // every 16 / 64 pops (C3 worker busy -20 %, wh10k 400 steps 5.77 -> 5.42 s; profiles/r3/dag_exit_ab.txt)
     W.dag_mask = c->tun.dag_mask ? c->tun.dag_mask : (W.dag == 1u ? 15u : 63u);
+    W.idle_ticks = c->tun.worker_idle_us * 100ull;  // wall clock: 100 MHz
     W.dist = c->d_dist;
     W.gs_lds = wcfg.gs_lds;
     W.stage_fb = wcfg.stage_fb;
@@ -1314,7 +1317,15 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
         resume.qcount = 0;
         return run_plan_impl(c, P, resume);
       }
-      continue;  // the workers resolved every needed pair before exiting: relaunch
+      // the planner gave up waiting (no worker left — they exit after an idle spell — or a pair stayed
+      // pending): resolve its needed queue on the host side before relaunching, so every relaunch makes
+      // progress whatever the workers of the next dispatch do (exact codes; resolved ones rewrite the same)
+      if (k.qcount > 0) {
+        if (k.qcount > P.qcap) RET(TSW_EINVAL, "plan kernel queue overflow");
+        TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
+        TRY(check_err(c));
+      }
+      continue;
     }
     if (k.status != PLAN_NEED_QUERIES || k.qcount == 0 || k.qcount > P.qcap)
       RET(TSW_EINVAL, "plan kernel stopped without resolvable next hops");

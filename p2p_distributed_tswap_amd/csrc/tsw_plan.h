@@ -139,6 +139,7 @@ struct WorkerArgs {
   uint32_t dag;
   const uint16_t* dist;  // K1 tables, nstride entries per goal slot
   uint32_t dag_mask;     // the DAG test runs when (pops & dag_mask) == 0
+  unsigned long long idle_ticks;  // a worker idle this long (100 MHz ticks) exits (5 s)
 };
 // Worker placement: per-wave LDS (heap, g-scores, free bitmap) sets the waves per CU. g-scores stay
 // in LDS (fastest per pop) unless that leaves < 3 waves per CU while many agents can need queries at

@@ -48,7 +48,8 @@ __device__ __forceinline__ uint32_t hw_xcc_id() {
 // lane 0: claim the next pair (0: needed queue, 1: speculative queue, 2: task chain, -1: exit).
 // Task chains (long, lowest priority) only go to workers with take_t: the others stay free for the
 // pairs the planner needs or will need soon.
-__device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags) {
+__device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags,
+                                            unsigned long long idle_ticks) {
   const unsigned long long t0 = wall_clock64();
   // one pass over the queues in priority order: >= 0 claimed (queue id), -1 nothing, -2 stop
   auto scan = [&]() -> int {
@@ -102,7 +103,7 @@ __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool tak
       if ((k & 255u) == 255u && hflags &&
           __hip_atomic_load(&hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
         return -1;
-      if (wall_clock64() - t0 > 500000000ull) return -1;  // 5 s idle: safety exit
+      if (wall_clock64() - t0 > idle_ticks) return -1;  // idle this long (5 s): safety exit
       if (k < 8) __builtin_amdgcn_s_sleep(2);
       else __builtin_amdgcn_s_sleep(16);
       const uint32_t p = w_ld(&cc->pub);
@@ -274,7 +275,7 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   for (;;) {
     int which = -1;
     uint32_t idx = 0;
-    if (lane == 0) which = worker_claim(A.cc, &idx, take_t, A.hflags);
+    if (lane == 0) which = worker_claim(A.cc, &idx, take_t, A.hflags, A.idle_ticks);
     which = __builtin_amdgcn_readfirstlane(which);
     if (which < 0) break;
     idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);

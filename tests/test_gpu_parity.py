@@ -406,3 +406,15 @@ def test_mapd_partial_lds_agent_arrays(monkeypatch, mask):
     rows = maps.random_map(128, 128, 0.1, 0x6000)
     starts, tasks = maps.make_instance(rows, 6000, 600, 0x6001)
     _plan_vs_oracle(rows, starts, tasks, 30, diag=True)
+
+
+def test_mapd_workers_leave_when_idle(monkeypatch):
+    """coop workers that all leave (idle timeout cut to 20 us, TSW_WORKER_IDLE_US) while the
+    planner still needs pairs: the planner sees `alive == 0`, stops waiting within ~1 ms, the call
+    relaunches with fresh workers, and the C3 prefix stays bit-exact."""
+    monkeypatch.setenv("TSW_WORKER_IDLE_US", "20")
+    monkeypatch.setenv("TSW_TASK_CHAINS", "0")  # no long chain jobs keeping workers busy
+    rows, starts, tasks = maps.config_instance("c3_warehouse_170x84")
+    st = _plan_vs_oracle(rows, starts, tasks, 150, diag=True)
+    assert st["coop_workers"] > 0 and st["watchdog_fires"] == 0
+    assert st["walker_launches"] >= 2, st["walker_launches"]  # the planner did give up on absent workers
