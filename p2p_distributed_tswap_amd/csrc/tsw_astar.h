@@ -420,49 +420,31 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
 
 // Detour bytes of a goal's K1 table for astar_wave_par<*, *, 1>: DT[c] = (D[c] - |c - goal|_1) / 2
 // (D and the Manhattan distance share parity on a 4-grid), 255 when that is >= 255 or c is blocked /
-// unreachable. One wave; D is the slot's u16 table (16-B aligned, >= round8(ncell) entries), DT holds
-// round8(ncell) bytes. Lane l converts cells 8l .. 8l+7 of each 512-cell chunk, four chunks per round
-// with their loads issued together (the table comes from HBM: one latency per round, not per chunk).
-__device__ __forceinline__ void stage_detour(uint8_t* DT, const uint16_t* D, uint32_t ncell, uint32_t W,
-                                             uint32_t goal, uint32_t lane) {
+// unreachable. One wave; D is the slot's u16 table. Only the cells of the box [x0, x1] x [y0, y1] are
+// written: the caller passes the bounding box of the query's ellipse {x : |x - v| + |x - goal| <= d*},
+// outside which every cell has f = g + h > d* and so can never pass the DAG test (g + D = d*) whatever
+// DT holds there. Lanes walk the box's cells in row-major order, four loads in flight per lane.
+__device__ __forceinline__ void stage_detour(uint8_t* DT, const uint16_t* D, uint32_t W, uint32_t goal, uint32_t x0,
+                                             uint32_t x1, uint32_t y0, uint32_t y1, uint32_t lane) {
   const uint32_t gy = goal / W, gx = goal - gy * W;
-  const uint32_t n8 = (ncell + 7u) >> 3;
-  // (x, y) of this lane's first cell; each further chunk is 512 cells on
-  uint32_t y = (8u * lane) / W, x = 8u * lane - y * W;
-  const uint32_t sy = 512u / W, sx = 512u - sy * W;
-  const uint4* D4 = reinterpret_cast<const uint4*>(D);
-  for (uint32_t i0 = lane; i0 < n8; i0 += 256u) {
-    uint4 d4[4];
+  const uint32_t bw = x1 - x0 + 1u, nb = bw * (y1 - y0 + 1u);
+  const float inv = 1.0f / (float)bw;
+  for (uint32_t i0 = lane; i0 < nb; i0 += 256u) {
+    uint32_t cell[4], d[4], x[4], y[4];
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
       const uint32_t i = i0 + 64u * u;
-      d4[u] = i < n8 ? D4[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+      const uint32_t r = fast_div(i < nb ? i : 0u, bw, inv);
+      y[u] = y0 + r;
+      x[u] = x0 + ((i < nb ? i : 0u) - r * bw);
+      cell[u] = y[u] * W + x[u];
+      d[u] = D[cell[u]];
     }
 #pragma unroll
     for (uint32_t u = 0; u < 4; ++u) {
-      const uint32_t i = i0 + 64u * u;
-      const uint32_t dw[4] = {d4[u].x, d4[u].y, d4[u].z, d4[u].w};
-      uint32_t out[2] = {0u, 0u};
-      uint32_t cx = x, cy = y;
-#pragma unroll
-      for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t d = (dw[k >> 1] >> (16u * (k & 1u))) & 0xFFFFu;
-        const uint32_t man = (cx > gx ? cx - gx : gx - cx) + (cy > gy ? cy - gy : gy - cy);
-        const uint32_t det = d == 0xFFFFu || d < man ? 255u : min((d - man) >> 1, 255u);
-        out[k >> 2] |= det << (8u * (k & 3u));
-        if (++cx == W) {
-          cx = 0;
-          ++cy;
-        }
-      }
-      if (i < n8) reinterpret_cast<uint2*>(DT)[i] = make_uint2(out[0], out[1]);
-      // next chunk of this lane: 512 cells on
-      x += sx;
-      y += sy;
-      if (x >= W) {
-        x -= W;
-        ++y;
-      }
+      if (i0 + 64u * u >= nb) break;
+      const uint32_t man = (x[u] > gx ? x[u] - gx : gx - x[u]) + (y[u] > gy ? y[u] - gy : gy - y[u]);
+      DT[cell[u]] = (uint8_t)(d[u] == 0xFFFFu || d[u] < man ? 255u : min((d[u] - man) >> 1, 255u));
     }
   }
 }

@@ -177,9 +177,10 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     for (uint32_t t = lane; t < nfw; t += 64u) fb[t] = G.freebits[t];
     FB = fb;
   }
-  // DAG early exit (A.dag == 1): the detour bytes of the goal last staged (dt_goal), after the bitmap
+  // DAG early exit (A.dag == 1): the detour bytes of the goal last staged (dt_goal) over the box
+  // dt_box = x0 | x1 << 16 (dt_bx), y0 | y1 << 16 (dt_by), after the bitmap
   uint8_t* DT = reinterpret_cast<uint8_t*>(wsm + hcap) + gsb + (A.stage_fb ? (nfw * 4u + 15u) / 16u * 16u : 0u);
-  uint32_t dt_goal = 0xFFFFFFFFu;
+  uint32_t dt_goal = 0xFFFFFFFFu, dt_bx = 0u, dt_by = 0u;
   if (gs_lds == 1u)
     for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
   uint32_t* GSg = A.gs_all + (uint64_t)wid * ncell;
@@ -196,15 +197,32 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     int32_t L = 0;
     uint8_t code = NH_UNKNOWN;
     uint32_t np = 0, npt = 0;  // heap pops (diagnostics)
-    const uint32_t dag = tab >= 0 ? A.dag : 0u;
+    uint32_t dag = tab >= 0 ? A.dag : 0u;
     const uint16_t* DGt = dag ? A.dist + (uint64_t)tab * A.nstride : nullptr;
-    if (dag == 1u && dt_goal != goal) {
-      const unsigned long long ts0 = wall_clock64();
-      stage_detour(DT, DGt, ncell, G.W, goal, lane);
-      dt_goal = goal;
-      if (lane == 0) {  // diagnostics: staging time / count
-        __hip_atomic_fetch_add(&A.cc->wbusy[3], wall_clock64() - ts0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&A.cc->wcount[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dag == 1u) {
+      // the query's ellipse box: d* = D[v], margin (d* - |v - goal|) / 2 around the start/goal box
+      const uint32_t W = G.W, vy = v / W, vx = v - vy * W, gy = goal / W, gx = goal - gy * W;
+      const uint32_t ds = __builtin_amdgcn_readfirstlane((uint32_t)DGt[v]);
+      const uint32_t man = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
+      if (ds == 0xFFFFu || ds > 508u || ds < man) {
+        dag = 0u;  // unreachable or detour past the byte range: the full search
+      } else {
+        const uint32_t e = (ds - man) >> 1;
+        const uint32_t x0 = min(vx, gx) > e ? min(vx, gx) - e : 0u, x1 = min(max(vx, gx) + e, W - 1u);
+        const uint32_t y0 = min(vy, gy) > e ? min(vy, gy) - e : 0u, y1 = min(max(vy, gy) + e, G.H - 1u);
+        const bool inside = dt_goal == goal && x0 >= (dt_bx & 0xFFFFu) && x1 <= (dt_bx >> 16) &&
+                            y0 >= (dt_by & 0xFFFFu) && y1 <= (dt_by >> 16);
+        if (!inside) {
+          const unsigned long long ts0 = wall_clock64();
+          stage_detour(DT, DGt, W, goal, x0, x1, y0, y1, lane);
+          dt_goal = goal;
+          dt_bx = x0 | (x1 << 16);
+          dt_by = y0 | (y1 << 16);
+          if (lane == 0) {  // diagnostics: staging time / count
+            __hip_atomic_fetch_add(&A.cc->wbusy[3], wall_clock64() - ts0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&A.cc->wcount[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
       }
     }
     if (gs_lds == 2u) {
