@@ -1285,8 +1285,11 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                   "MOVE %u/%u | PRE1 never queued: assigned %u, picked up %u | chain queries %llu of %llu\n", cc.dbg_need[0], cc.dbg_need[1], cc.dbg_need[2],
                   cc.dbg_need[3], cc.dbg_need[4], cc.dbg_need[5], cc.dbg_need[6], cc.dbg_need[7],
                   (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
-          fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u\n",
-                  cc.waits ? (double)cc.dbg_depth / cc.waits : 0.0, cc.dbg_depth_max);
+          fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u | queue delay enqueue -> claim: needed "
+                  "avg %.1f us (%u > 1 ms, %u already resolved), speculative avg %.1f us (%u > 1 ms, %u already resolved)\n",
+                  cc.waits ? (double)cc.dbg_depth / cc.waits : 0.0, cc.dbg_depth_max,
+                  cc.wcount[0] ? cc.qdelay[0] / 100.0 / cc.wcount[0] : 0.0, cc.qlate[0], cc.qskip[0],
+                  cc.wcount[1] ? cc.qdelay[1] / 100.0 / cc.wcount[1] : 0.0, cc.qlate[1], cc.qskip[1]);
           fprintf(stderr, "[k_plan] worker A* ms (queries, pops): needed %.1f (%u, %llu) spec %.1f (%u, %llu) task chains "
                   "%.1f (%u, %llu) | tier-2 hand-offs %llu tier-3 %llu | detour staging %.1f ms (%u)\n",
                   cc.wbusy[0] / (double)c->wall_khz, cc.wcount[0], cc.wpops[0], cc.wbusy[1] / (double)c->wall_khz,

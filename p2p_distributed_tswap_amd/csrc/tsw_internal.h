@@ -85,6 +85,9 @@ struct CoopCtl {
   unsigned long long wbusy[4];
   uint32_t wcount[4];
   unsigned long long wpops[4];  // ... and heap pops (all tiers)
+  unsigned long long qdelay[2];  // diagnostics: enqueue -> claim wall ticks, needed / speculative queue
+  uint32_t qlate[2];             // ... claims later than 1 ms after the enqueue
+  uint32_t qskip[2];             // claimed pairs already resolved when claimed (not searched again)
   // diagnostics: speculative-queue backlog (published - claimed) when a planner wait starts
   unsigned long long dbg_depth;
   uint32_t dbg_depth_max, pad4[3];

@@ -270,7 +270,8 @@ __device__ __forceinline__ void put_query(const PlanArgs& P, uint8_t* p, uint32_
   q.v = v;
   q.goal = g;
   q.tab = tab;
-  q.out = qi;
+  // coop mode reads no result index: the entry carries its enqueue time (wall clock, low 32 bits)
+  q.out = P.coop ? (uint32_t)wall_clock64() : qi;
   P.Q[qi] = q;
 }
 
@@ -308,7 +309,7 @@ __device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uin
     q.v = v;
     q.goal = g;
     q.tab = tab;
-    q.out = qi;
+    q.out = (uint32_t)wall_clock64();  // enqueue time (diagnostics)
     P.QS[qi] = q;
     return;
   }

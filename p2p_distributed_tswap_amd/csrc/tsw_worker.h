@@ -304,6 +304,17 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     const int32_t tab = (int32_t)w_ld(e + 2);
     cur_q = (uint32_t)which;
     if (which < 2) {
+      // a pair resolved meanwhile (a promoted speculative pair whose first copy finished, or a chain
+      // hop) is not searched again
+      if (tab >= 0 && (uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(v, tab) : 0u) <= NH_STAY) {
+        if (lane == 0) __hip_atomic_fetch_add(&A.cc->qskip[which], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
+      if (lane == 0) {  // diagnostics: queue delay (enqueue time in the entry's out word)
+        const uint32_t dt = (uint32_t)wall_clock64() - w_ld(e + 3);
+        __hip_atomic_fetch_add(&A.cc->qdelay[which], (unsigned long long)dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dt > 100000u) __hip_atomic_fetch_add(&A.cc->qlate[which], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       publish_code(v, tab, resolve(v, goal, tab), false);
       continue;
     }
