@@ -61,7 +61,8 @@ struct Tables {
 };
 
 // Concurrent K3 (coop mode): the planner publishes queued pairs, persistent A* worker waves on the
-// other CUs claim and resolve them while the planner keeps running (tsw_plan.hip, k_astar_worker).
+// other CUs — workgroups 1.. of the same k_plan dispatch — claim and resolve them while the planner keeps
+// running (tsw_worker.h).
 // Counters live on separate 128-B lines (claimed by CAS from many CUs, polled by the planner).
 struct CoopCtl {
   uint32_t head_n, pad0[31];   // needed queue: entries published by the planner

@@ -84,7 +84,7 @@ struct PlanArgs {
   PlanCtl* ctl;
   unsigned long long* sec_ticks;  // [16] wall-clock ticks per section [0..7] and sub-phase [8..15] (diagnostics)
   uint32_t dbg;                   // sub-phase ticks on (TSW_PLAN_DEBUG)
-  // coop mode: K3 runs concurrently in k_astar_worker; Q is the needed queue (qcap entries for the
+  // coop mode: K3 runs concurrently in the dispatch's worker workgroups (tsw_worker.h); Q is the needed queue (qcap entries for the
   // whole launch), QS the speculative one; missing next hops are waited for instead of exiting
   uint32_t coop;
   AstarQuery* QS;
