@@ -1,0 +1,45 @@
+"""Planner-only time of a plan: the same C3 (or other) plan twice in one context, the second time with
+every next-hop code the first one resolved still in the table store (no K3 waits), vs cold plans from
+an empty store. cold - warm = what the A* latency chain costs the plan.
+
+usage: python scripts/warm_plan.py [--config c3_warehouse_170x84] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from p2p_distributed_tswap_amd import Planner, maps  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3_warehouse_170x84")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    rows, starts, tasks = maps.config_instance(a.config)
+    out = {"config": a.config, "cold_ms": [], "warm_ms": [], "warm_waits": [], "cold_waits": []}
+    with Planner(rows) as p:
+        p.plan_mapd_arrays(starts, tasks, 50)
+        for _ in range(a.reps):
+            p.clear_tables()
+            p.reset_stats()
+            t0 = time.perf_counter()
+            ref, _ = p.plan_mapd_arrays(starts, tasks, 2000)
+            out["cold_ms"].append(round(1e3 * (time.perf_counter() - t0), 2))
+            out["cold_waits"].append(p.stats()["coop_waits"])
+            p.reset_stats()
+            t0 = time.perf_counter()
+            rec, _ = p.plan_mapd_arrays(starts, tasks, 2000)
+            out["warm_ms"].append(round(1e3 * (time.perf_counter() - t0), 2))
+            out["warm_waits"].append(p.stats()["coop_waits"])
+            assert (rec == ref).all()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
