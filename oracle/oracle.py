@@ -48,6 +48,9 @@ def lib():
         L.orc_decide.argtypes = [ctypes.c_void_p, u32, u32, P(u32), P(u32), u32, P(u32), P(u32), P(u32), P(u32),
                                  P(u32)]
         L.orc_decide.restype = ctypes.c_int
+        L.orc_tswap_mapd_fast.argtypes = [P(ctypes.c_uint8), u32, u32, P(u32), u32, P(u32), u32, u32, P(u64),
+                                          P(u32), u32, P(u64)]
+        L.orc_tswap_mapd_fast.restype = i32
         L.orc_stat_calls.argtypes = [ctypes.c_void_p]
         L.orc_stat_calls.restype = u64
         L.orc_stat_pops.argtypes = [ctypes.c_void_p]
@@ -112,6 +115,24 @@ class OracleGraph:
         if T < 0:
             raise ValueError("invalid input (reference would panic)")
         return out[:n, :T], (gout[:n, :T] if gout is not None else None)
+
+    def mapd_fast(self, starts_xy: np.ndarray, tasks_xyxy: np.ndarray, max_t: int = 2000, nthreads: int = 8):
+        """Same plan as mapd(trace_goals=True) from the memoised, prefilled oracle loop
+        (tswap_oracle_fast.c). Returns (rec, goals, stats) with stats = {inline, prefill, hits, memo}."""
+        s = np.ascontiguousarray(starts_xy, dtype=np.uint32).reshape(-1)
+        t = np.ascontiguousarray(tasks_xyxy, dtype=np.uint32).reshape(-1)
+        n, m = s.size // 2, t.size // 4
+        out = np.zeros((max(n, 1), max_t + 1), dtype=np.uint64)
+        gout = np.zeros((max(n, 1), max_t + 1), dtype=np.uint32)
+        st = np.zeros(4, dtype=np.uint64)
+        T = lib().orc_tswap_mapd_fast(self.cells.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), self.w, self.h,
+                                      _u32p(s), n, _u32p(t), m, max_t,
+                                      out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _u32p(gout), nthreads,
+                                      st.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+        if T < 0:
+            raise ValueError("invalid input (reference would panic)")
+        stats = dict(zip(("inline", "prefill", "hits", "memo"), (int(x) for x in st)))
+        return out[:n, :T], gout[:n, :T], stats
 
     def decide(self, my_v: int, my_g: int, nb_v, nb_g):
         """compute_next_move_with_tswap (agent.rs:329-462) for one agent. Returns

@@ -386,9 +386,11 @@ int32_t orc_tswap_mapd(orc_graph *gr, const uint32_t *starts_xy, uint32_t n,
         st[i] = ST_IDLE;
         task_of[i] = -1;
     }
+    /* task cells are looked up only when used: pickup at assignment (:136), delivery on reaching the
+     * pickup (:112) — an off-grid/blocked one panics there, not before */
     for (uint32_t k = 0; k < m; k++) {
-        if (xy_to_cell(gr, tasks_xyxy[4 * k], tasks_xyxy[4 * k + 1], &pick[k])) goto out;
-        if (xy_to_cell(gr, tasks_xyxy[4 * k + 2], tasks_xyxy[4 * k + 3], &dlv[k])) goto out;
+        if (xy_to_cell(gr, tasks_xyxy[4 * k], tasks_xyxy[4 * k + 1], &pick[k])) pick[k] = UINT32_MAX;
+        if (xy_to_cell(gr, tasks_xyxy[4 * k + 2], tasks_xyxy[4 * k + 3], &dlv[k])) dlv[k] = UINT32_MAX;
     }
     uint32_t unused = m;
     uint32_t timestep = 0;
@@ -399,7 +401,10 @@ int32_t orc_tswap_mapd(orc_graph *gr, const uint32_t *starts_xy, uint32_t n,
             if (v[i] == g[i]) {
                 if (st[i] == ST_TO_PICKUP) {
                     st[i] = ST_TO_DELIVERY;
-                    if (task_of[i] >= 0) g[i] = dlv[task_of[i]];
+                    if (task_of[i] >= 0) {
+                        if (dlv[task_of[i]] == UINT32_MAX) goto out; /* pos2id[&task.delivery] panics */
+                        g[i] = dlv[task_of[i]];
+                    }
                 } else if (st[i] == ST_TO_DELIVERY) {
                     st[i] = ST_IDLE;
                     task_of[i] = -1;
@@ -424,6 +429,7 @@ int32_t orc_tswap_mapd(orc_graph *gr, const uint32_t *starts_xy, uint32_t n,
                     unused--;
                     task_of[i] = best;
                     st[i] = ST_TO_PICKUP;
+                    if (pick[best] == UINT32_MAX) goto out; /* pos2id[&task.pickup] panics */
                     g[i] = pick[best];
                 }
             }

@@ -60,8 +60,11 @@ int orc_tswap_step(orc_graph *gr, uint32_t *v, uint32_t *g, uint32_t n);
  * goal_out (optional, same shape, u32 cell id of g after the step) is a debug
  * trace for localising divergences. The reference's step cap is
  * `timestep > 2000` (tswap.rs:167); max_t generalises the 2000.
- * Returns number of recorded timesteps T, or <0 on invalid input (the
- * reference would panic, tswap.rs:94,112,136). */
+ * Returns number of recorded timesteps T, or <0 on invalid input where the
+ * reference panics: an off-grid/blocked start (tswap.rs:94, checked up front), a
+ * task whose off-grid/blocked pickup is assigned (:136) or whose off-grid/blocked
+ * delivery is looked up on reaching the pickup (:112). A bad task cell that is
+ * never looked up does not fail the call, as in the reference. */
 int32_t orc_tswap_mapd(orc_graph *gr, const uint32_t *starts_xy, uint32_t n,
                        const uint32_t *tasks_xyxy, uint32_t m, uint32_t max_t,
                        uint64_t *rec_out, uint32_t *goal_out);
