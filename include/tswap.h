@@ -125,7 +125,12 @@ const char *tsw_last_error(const tsw_ctx *ctx);
  * out: caller-allocated n*(max_t+1) records, agent-major:
  *   out[i*(max_t+1) + t] == paths[i][t]  for t < *out_T.
  * max_t = 2000 reproduces the reference's `timestep > 2000` stop (:167).
- * Returns TSW_EINVAL if a start, pickup or delivery is off-grid or blocked. */
+ * Returns TSW_EINVAL where the reference panics: a start off-grid or blocked
+ * (checked up front, :94), a task whose off-grid/blocked pickup gets assigned
+ * (:136), or whose off-grid/blocked delivery is looked up when its agent reaches
+ * the pickup (:112). A bad task cell that is never looked up does not fail the
+ * call. The nearest-pickup choice uses the raw pickup point (:125-130), its
+ * coordinates clamped to 0xFFFF (cannot change the winner: see tsw_capi.hip). */
 int tsw_plan_mapd(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const tsw_task *tasks,
                   uint32_t m, uint32_t max_t, tsw_rec *out, uint32_t *out_T);
 

@@ -50,7 +50,7 @@ enum { CAT_BFS = 0, CAT_ASTAR = 1, CAT_WALK = 2, CAT_ASSIGN = 3, NCAT = 4 };
 // variables below ONCE when a context is created — kernel A/B variants, instrumentation, and
 // TSW_BFS_DBG, which drops work and writes WRONG tables (measurement only).
 struct Tunables {
-  uint32_t bfs_mode = 0;          // TSW_BFS_KERNEL: 0 auto, 1 wave (row words), 2 block, 3 blk (8x8), 4 big
+  uint32_t bfs_mode = 0;          // TSW_BFS_KERNEL: 0 auto, 1 wave (row words), 2 block, 3 blk (8x8), 4 big, 5 mg
   uint32_t bfs_cap = 512;         // TSW_BFS_LISTCAP: k_bfs_wave LDS list entries
   uint32_t blk_cap = 576;         // TSW_BFS_BLKCAP: k_bfs_blk LDS list entries
   uint32_t bfs_waves = 16;        // TSW_BFS_WAVES: waves per K1 workgroup cap
@@ -92,7 +92,7 @@ struct Tunables {
       return std::max(lo, std::min(hi, atol(v)));
     };
     if (const char* m = getenv("TSW_BFS_KERNEL"))
-      t.bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : !strcmp(m, "blk") ? 3u : !strcmp(m, "big") ? 4u : 0u;
+      t.bfs_mode = !strcmp(m, "wave") ? 1u : !strcmp(m, "block") ? 2u : !strcmp(m, "blk") ? 3u : !strcmp(m, "big") ? 4u : !strcmp(m, "mg") ? 5u : 0u;
     t.bfs_cap = (uint32_t)num("TSW_BFS_LISTCAP", 1, 32768, t.bfs_cap);
     t.blk_cap = (uint32_t)num("TSW_BFS_BLKCAP", 1, 32768, t.blk_cap);
     t.bfs_waves = (uint32_t)num("TSW_BFS_WAVES", 1, 16, t.bfs_waves);
@@ -150,6 +150,14 @@ struct tsw_ctx {
   uint64_t* d_frb = nullptr;
   uint32_t* d_abase = nullptr;  // k_bfs_blk run-start numbering
   uint32_t nrs = 0;
+  uint32_t nfree = 0;                   // free cells (k_bfs_mg: u16 levels need <= 65535)
+  // K1 v5 (k_bfs_mg): goal groups of the current launch order (bfs_order), per-workgroup scratch
+  std::vector<uint32_t> h_mg_grp;
+  uint32_t* d_mg_grp = nullptr;
+  size_t mg_grp_cap = 0;
+  uint32_t* d_mg_wl = nullptr;
+  uint16_t* d_mg_anch = nullptr;
+  uint32_t mg_wgs = 0;
   unsigned long long* d_wlg = nullptr;  // k_bfs_blk per-wave WL scratch
   uint64_t wlg_waves = 0;
   uint16_t* d_anch = nullptr;
@@ -382,7 +390,69 @@ int ensure_tmp(tsw_ctx* c, size_t k) {
 // wave of goals is the short ones (LPT scheduling) instead of a few long ones running on an
 // otherwise idle chip. Output positions are carried in `slots`. TSW_BFS_ORDER=0 keeps the
 // caller's order (A/B).
-void bfs_lpt_order(const tsw_ctx* c, std::vector<uint32_t>& goals, std::vector<uint32_t>& slots) {
+// k_bfs_mg serves this launch: its LDS layout fits, levels fit u16 (<= 65535 free cells), and the
+// batch is large enough to fill groups (mode 5 forces it whenever it fits)
+bool mg_selected(const tsw_ctx* c, size_t k) {
+  if (c->tun.bfs_mode != 0u && c->tun.bfs_mode != 5u) return false;
+  if (c->nfree > 0xFFFFu || c->nbp > 0xFFFFu || c->max_lds <= 0) return false;
+  if (bfs_mg_lds_bytes(c->G.W, c->G.H, c->nbp) > (size_t)c->max_lds) return false;
+  return c->tun.bfs_mode == 5u || k >= 64u;
+}
+
+uint32_t morton2(uint32_t x, uint32_t y) {
+  uint32_t z = 0;
+  for (uint32_t b = 0; b < 16u; ++b) z |= ((x >> b) & 1u) << (2u * b) | ((y >> b) & 1u) << (2u * b + 1u);
+  return z;
+}
+
+// k_bfs_mg launch order: goals grouped by (cell parity, Morton order) into groups of <= 16 (one
+// parity per group: the kernel advances all of a group's fronts on one checkerboard colour per
+// level), groups ordered longest-first by the eccentricity bound of their first goal (LPT, as
+// bfs_lpt_order). Fills c->h_mg_grp with the group offsets.
+void bfs_mg_order(tsw_ctx* c, std::vector<uint32_t>& goals, std::vector<uint32_t>& slots) {
+  const uint32_t W = c->G.W, H = c->G.H;
+  const size_t k = goals.size();
+  std::vector<std::pair<uint64_t, uint32_t>> key(k);
+  for (size_t i = 0; i < k; ++i) {
+    const uint32_t y = goals[i] / W, x = goals[i] - y * W;
+    key[i] = {((uint64_t)((x + y) & 1u) << 40) | morton2(x, y), (uint32_t)i};
+  }
+  std::sort(key.begin(), key.end());
+  std::vector<std::pair<uint32_t, uint32_t>> grp;  // (start, end) in key order
+  for (size_t i = 0; i < k;) {
+    size_t j = i + 1;
+    while (j < k && j - i < 16u && (key[j].first >> 40) == (key[i].first >> 40)) ++j;
+    grp.push_back({(uint32_t)i, (uint32_t)j});
+    i = j;
+  }
+  auto ecc = [&](uint32_t g) {
+    const uint32_t y = g / W, x = g - y * W;
+    return std::max(x, W - 1 - x) + std::max(y, H - 1 - y);
+  };
+  std::stable_sort(grp.begin(), grp.end(), [&](const auto& a, const auto& b) {
+    return ecc(goals[key[a.first].second]) > ecc(goals[key[b.first].second]);
+  });
+  std::vector<uint32_t> g2, s2;
+  g2.reserve(k);
+  s2.reserve(k);
+  c->h_mg_grp.assign(1, 0u);
+  for (const auto& gr : grp) {
+    for (uint32_t i = gr.first; i < gr.second; ++i) {
+      g2.push_back(goals[key[i].second]);
+      s2.push_back(slots[key[i].second]);
+    }
+    c->h_mg_grp.push_back((uint32_t)g2.size());
+  }
+  goals.swap(g2);
+  slots.swap(s2);
+}
+
+void bfs_lpt_order(tsw_ctx* c, std::vector<uint32_t>& goals, std::vector<uint32_t>& slots) {
+  c->h_mg_grp.clear();
+  if (mg_selected(c, goals.size())) {
+    bfs_mg_order(c, goals, slots);
+    return;
+  }
   if (!c->tun.bfs_order || goals.size() < 2) return;
   const uint32_t W = c->G.W, H = c->G.H, maxe = W + H;
   // counting sort by eccentricity bound, descending, stable: O(k + W + H) on the host
@@ -633,6 +703,58 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
   const bool vec16 = c->G.W % 8u == 0u && dstride % 8u == 0u && ((uintptr_t)dist & 15u) == 0u;
   const uint32_t max_waves = c->tun.bfs_waves;
   const uint32_t bfs_mode = c->tun.bfs_mode;
+  if (mg_selected(c, k) && !c->h_mg_grp.empty() && c->h_mg_grp.back() == k) {
+    // goal-bit-parallel groups (the launch order came from bfs_mg_order)
+    Timer t(c, CAT_BFS);
+    const uint32_t ngroups = (uint32_t)c->h_mg_grp.size() - 1u;
+    const uint32_t wlw = (c->G.ncell + 1u) / 2u;
+    const uint32_t wgs = (uint32_t)std::max(c->num_cu, 1);
+    if (c->mg_wgs < wgs || !c->d_mg_wl) {
+      HIPCHK(hipStreamSynchronize(c->s));
+      if (c->d_mg_wl) HIPCHK(hipFree(c->d_mg_wl));
+      if (c->d_mg_anch) HIPCHK(hipFree(c->d_mg_anch));
+      c->d_mg_wl = nullptr;
+      c->d_mg_anch = nullptr;
+      c->mg_wgs = 0;
+      HIPCHK(hipMalloc(&c->d_mg_wl, (size_t)wgs * wlw * 4u));
+      HIPCHK(hipMalloc(&c->d_mg_anch, (size_t)wgs * std::max<uint32_t>(c->nrs, 1u) * 16u * 2u));
+      c->mg_wgs = wgs;
+    }
+    if (c->h_mg_grp.size() > c->mg_grp_cap || !c->d_mg_grp) {
+      HIPCHK(hipStreamSynchronize(c->s));
+      HIPCHK(dgrow(c->d_mg_grp, c->mg_grp_cap, c->h_mg_grp.size()));
+    }
+    HIPCHK(hipMemcpyAsync(c->d_mg_grp, c->h_mg_grp.data(), c->h_mg_grp.size() * 4u, hipMemcpyHostToDevice, c->s));
+    MgBfsArgs A{};
+    A.W = c->G.W;
+    A.H = c->G.H;
+    A.Bp = c->Bp;
+    A.nbp = c->nbp;
+    A.frb = c->d_frb;
+    A.abase = c->d_abase;
+    A.nrs = std::max<uint32_t>(c->nrs, 1u);
+    A.goals = goals;
+    A.slots = slots;
+    A.grp = c->d_mg_grp;
+    A.ngroups = ngroups;
+    A.dist = dist;
+    A.dstride = dstride;
+    A.wl = c->d_mg_wl;
+    A.wlw = wlw;
+    A.anch = c->d_mg_anch;
+    A.work = &c->d_stat->work;
+    A.err = &c->d_stat->err;
+    A.scratch_wgs = c->mg_wgs;
+    A.prof = (uint64_t*)bfs_prof_buf(c);
+    HIPCHK(hipMemsetAsync(&c->d_stat->work, 0, 4, c->s));
+    HIPCHK(launch_bfs_mg(A, c->max_lds, c->num_cu, c->s));
+    // the host copy of the group offsets must outlive the async upload
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (A.prof) TRY(bfs_prof_print(c, "k_bfs_mg", k));
+    if (nh) HIPCHK(launch_classify(c->G, goals, slots, k, dist, dstride, nh, c->s));
+    return TSW_OK;
+  }
+  if (bfs_mode == 5) RET(TSW_EINVAL, "k_bfs_mg does not fit this grid (forced kernel mg)");
   uint32_t nbw = 0;
   // two goals per wave only where two goal slots per wave fit LDS, else one
   bool pair = c->tun.bfs_pair != 0u;
@@ -1255,6 +1377,10 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                "%u move rounds", c->watchdog_ms, k.t, k.section, k.i, k.rule_rounds, k.move_rounds);
       RET(TSW_EINVAL, buf);
     }
+    if (k.err & ERR_BAD_PICKUP)
+      RET(TSW_EINVAL, "assigned task's pickup is off-grid or blocked (reference panics at tswap.rs:136)");
+    if (k.err & ERR_BAD_DELIVERY)
+      RET(TSW_EINVAL, "reached pickup's task delivery is off-grid or blocked (reference panics at tswap.rs:112)");
     if (k.err) {
       char buf[128];
       snprintf(buf, sizeof buf, "plan kernel error bits 0x%x", k.err);
@@ -1356,14 +1482,18 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
       RET(TSW_EINVAL, "start position off-grid or blocked (reference panics at tswap.rs:94)");
     goalset.push_back(vcell[i]);
   }
+  // Task cells are looked up only when the planner needs them — the pickup when the task is
+  // assigned (pos2id[&task.pickup], tswap.rs:136), the delivery when its agent reaches the pickup
+  // (:112) — so an off-grid or blocked one fails the call only then (k_plan ERR_BAD_*), exactly
+  // where the reference panics. The assignment's Manhattan distance still uses the raw point
+  // (:125-130); coordinates are clamped to 16 bits, which cannot change which task wins: any point
+  // past 0xFFFF is farther than every on-grid pickup (sides <= 2048), and assigning it fails anyway.
   for (uint32_t k = 0; k < m; ++k) {
-    if (!cell_ok(c, tasks[k].pickup.x, tasks[k].pickup.y, &pick[k]))
-      RET(TSW_EINVAL, "task pickup off-grid or blocked (reference panics at tswap.rs:136)");
-    if (!cell_ok(c, tasks[k].delivery.x, tasks[k].delivery.y, &dlv[k]))
-      RET(TSW_EINVAL, "task delivery off-grid or blocked (reference panics at tswap.rs:112)");
-    pick_xy[k] = tasks[k].pickup.x | (tasks[k].pickup.y << 16);
-    goalset.push_back(pick[k]);
-    goalset.push_back(dlv[k]);
+    if (!cell_ok(c, tasks[k].pickup.x, tasks[k].pickup.y, &pick[k])) pick[k] = CELL_BAD;
+    if (!cell_ok(c, tasks[k].delivery.x, tasks[k].delivery.y, &dlv[k])) dlv[k] = CELL_BAD;
+    pick_xy[k] = std::min<uint32_t>(tasks[k].pickup.x, 0xFFFFu) | (std::min<uint32_t>(tasks[k].pickup.y, 0xFFFFu) << 16);
+    if (pick[k] != CELL_BAD) goalset.push_back(pick[k]);
+    if (dlv[k] != CELL_BAD) goalset.push_back(dlv[k]);
   }
   TRY(ensure_agents(c, std::max<uint32_t>(n, 1)));
   if (m > c->tcap || !c->d_used) {
@@ -1413,7 +1543,7 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
       std::vector<AstarQuery> qt;
       qt.reserve(m);
       for (uint32_t k = 0; k < m; ++k)
-        if (pick[k] != dlv[k]) qt.push_back(AstarQuery{pick[k], dlv[k], c->h_goal_tab[dlv[k]], 0u});
+        if (pick[k] != dlv[k] && pick[k] != CELL_BAD && dlv[k] != CELL_BAD) qt.push_back(AstarQuery{pick[k], dlv[k], c->h_goal_tab[dlv[k]], 0u});
       if (qt.size() > c->qtcap) {
         HIPCHK(hipStreamSynchronize(c->s));
         HIPCHK(dgrow(c->d_QT, c->qtcap, qt.size()));
@@ -1569,6 +1699,9 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
       nrs += (uint64_t)__builtin_popcountll(f & ~wf);
     }
     c->nrs = (uint32_t)nrs;
+    uint64_t nf = 0;
+    for (uint32_t p = 0; p < c->nbp; ++p) nf += (uint64_t)__builtin_popcountll(frb[p]);
+    c->nfree = (uint32_t)std::min<uint64_t>(nf, 0xFFFFFFFFull);
     if ((e = hipMalloc(&c->d_abase, (size_t)c->nbp * 4)) != hipSuccess) return fail("malloc abase", e);
     if ((e = hipMemcpy(c->d_abase, abase.data(), (size_t)c->nbp * 4, hipMemcpyHostToDevice)) != hipSuccess)
       return fail("copy abase", e);
@@ -1619,7 +1752,7 @@ void tsw_destroy(tsw_ctx* c) {
   if (c->h_dups) (void)hipHostFree(c->h_dups);
   fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
-  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_govf);
+  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->h_stat) hipHostFree(c->h_stat);

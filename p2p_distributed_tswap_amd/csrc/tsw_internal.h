@@ -110,5 +110,9 @@ constexpr uint32_t ERR_WALK_OVERFLOW = 16u;
 constexpr uint32_t ERR_BFS_LIST = 32u;     // k_bfs_wave: a queued word gained no cell (logic error)
 constexpr uint32_t ERR_DECIDE_LIST = 64u;  // k_decide: a nearby list longer than DEC_MAX_LIST
 constexpr uint32_t ERR_ABORT = 128u;       // k_plan: stopped by the host watchdog (no step for 10 s)
+constexpr uint32_t ERR_BAD_PICKUP = 256u;  // k_plan: assigned a task whose pickup is off-grid/blocked (tswap.rs:136)
+constexpr uint32_t ERR_BAD_DELIVERY = 512u;  // k_plan: reached a pickup whose delivery is off-grid/blocked (:112)
+// task cell that is off-grid or blocked: the reference panics only when the planner looks it up
+constexpr uint32_t CELL_BAD = 0xFFFFFFFFu;
 
 }  // namespace tsw

@@ -96,6 +96,30 @@ bool bfs_big_fits(uint32_t nbp, int max_lds, uint32_t* cap_out);
 uint32_t bfs_big_workgroups(uint32_t nbp, uint32_t cap, int num_cu);
 hipError_t launch_bfs_big(const BigBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
 
+// K1 v5 (tsw_bfs_mg.hip): one WORKGROUP per group of <= 16 same-parity goals, a u16 goal mask per
+// cell in LDS; blocks numbered as k_bfs_blk (frb, abase shared with it).
+struct MgBfsArgs {
+  uint32_t W, H, Bp, nbp;
+  const uint64_t* frb;    // [nbp] padded free-cell blocks
+  const uint32_t* abase;  // [nbp] first run-start index of block p
+  uint32_t nrs;           // run starts in the grid
+  const uint32_t* goals;  // grouped: group j = goals[grp[j] .. grp[j+1]), one cell parity, <= 16
+  const uint32_t* slots;  // table slot per goal (nullptr: slot = goal index)
+  const uint32_t* grp;    // [ngroups + 1] group offsets
+  uint32_t ngroups;
+  uint16_t* dist;
+  uint64_t dstride;
+  uint32_t* wl;           // per-workgroup west-step masks, wlw u32 (two cells' u16 each)
+  uint32_t wlw;
+  uint16_t* anch;         // per-workgroup run-start levels, nrs * 16 u16 each
+  uint32_t* work;         // group dequeue counter (zeroed before the launch)
+  uint32_t* err;
+  uint32_t scratch_wgs;   // workgroups the scratch buffers are sized for
+  uint64_t* prof;         // optional: [bfs cycles, decode cycles, levels] summed over groups
+};
+size_t bfs_mg_lds_bytes(uint32_t W, uint32_t H, uint32_t nbp);
+hipError_t launch_bfs_mg(const MgBfsArgs& A, int max_lds, int num_cu, hipStream_t s);
+
 hipError_t launch_classify(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                            const uint16_t* dist_base, uint64_t stride, uint8_t* nh_base, hipStream_t s);
 

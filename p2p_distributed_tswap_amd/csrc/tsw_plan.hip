@@ -652,7 +652,7 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
       if (tk >= 0 && (uint32_t)tk < P.m) {
         pc = S.G[k];
         dc = P.dlv[tk];
-        const int32_t dt = P.goal_tab[dc];
+        const int32_t dt = dc == CELL_BAD ? -1 : P.goal_tab[dc];
         if (dt >= 0 && pc != dc) {
           dtab = dt;
           if (P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) prefetch_pair(P, pc, dc, dt, s_q);
@@ -756,6 +756,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[32], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
+  __shared__ uint32_t s_bad;               // ASSIGN looked up an off-grid/blocked task cell
   __shared__ uint32_t s_nassign, s_npick;  // diagnostics: this step's assignments / pickup arrivals
   const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6, nwaves = bd >> 6;
   const uint32_t n = P.n, W = P.W;
@@ -917,8 +918,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     }
     if (sec == SEC_ASSIGN) {
       // ---- K4: state machine + task assignment (tswap.rs:106-139) -------------
-      if (tid == 0) s_nassign = s_npick = 0;
-      for (uint32_t base = 0; base < n; base += bd) {
+      if (tid == 0) s_nassign = s_npick = s_bad = 0;
+      __syncthreads();
+      for (uint32_t base = 0; base < n && !s_bad; base += bd) {
         const uint32_t i = base + tid;
         bool needy = false;
         if (i < n) {
@@ -941,7 +943,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         }
         __syncthreads();
         const uint32_t cnt = s_cnt;
-        for (uint32_t kk = 0; kk < cnt; ++kk) {
+        for (uint32_t kk = 0; kk < cnt && !s_bad; ++kk) {
           const uint32_t ai = list[kk];
           if (tid == 0) {
             const uint32_t v = S.V[ai];
@@ -954,9 +956,14 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                 const int32_t tk = P.task[ai];
                 if (tk >= 0) {
                   const uint32_t ng = P.dlv[tk];
-                  S.G[ai] = ng;
-                  S.GT[ai] = P.goal_tab[ng];
-                  S.NHC[ai] = NHC_DIRTY;
+                  if (ng == CELL_BAD) {  // pos2id[&task.delivery] panics (tswap.rs:112)
+                    atomicOr(&P.ctl->err, ERR_BAD_DELIVERY);
+                    s_bad = 1;
+                  } else {
+                    S.G[ai] = ng;
+                    S.GT[ai] = P.goal_tab[ng];
+                    S.NHC[ai] = NHC_DIRTY;
+                  }
                 }
               } else if (st == ST_TO_DELIVERY) {
                 st = ST_IDLE;
@@ -969,6 +976,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
             s_py = v / W;
           }
           __syncthreads();
+          if (s_bad) break;  // block-uniform: the reference panicked on this agent
           if (s_doit) {
             const uint32_t px = s_px, py = s_py;
             uint64_t best = ~0ull;
@@ -997,14 +1005,27 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                 ++s_nassign;
                 if (P.dbg) S.DEC[ai] = 0x40;
                 const uint32_t ng = P.pick[t];
-                S.G[ai] = ng;
-                S.GT[ai] = P.goal_tab[ng];
-                S.NHC[ai] = NHC_DIRTY;
+                if (ng == CELL_BAD) {  // pos2id[&task.pickup] panics (tswap.rs:136)
+                  atomicOr(&P.ctl->err, ERR_BAD_PICKUP);
+                  s_bad = 1;
+                } else {
+                  S.G[ai] = ng;
+                  S.GT[ai] = P.goal_tab[ng];
+                  S.NHC[ai] = NHC_DIRTY;
+                }
               }
             }
           }
           __syncthreads();
         }
+      }
+      if (s_bad) {  // block-uniform: stop with the error bit set, no record for this timestep
+        if (tid == 0) {
+          s_ctl.status = PLAN_ERROR;
+          s_exit = 1;
+        }
+        __syncthreads();
+        break;
       }
       if (tid == 0) {
         s_ctl.section = SEC_PRE1;

@@ -1,4 +1,5 @@
-"""K1 parity: the four BFS kernels (k_bfs_blk: one wavefront per goal over 8x8 blocks;
+"""K1 parity: the five BFS kernels (k_bfs_mg: one workgroup per group of <= 16 same-parity goals,
+goal-bit-parallel; k_bfs_blk: one wavefront per goal over 8x8 blocks;
 k_bfs_wave: one wavefront per goal over row words; k_bfs: one workgroup per goal over row words;
 k_bfs_big: one workgroup per goal over 8x8 blocks, the large-grid kernel) against the oracle's BFS (oracle/tswap_oracle.c, cross-checked against A* path lengths in
 test_oracle.py), bit-exact, on ragged widths, list-overflow paths and the full-size den520d-like
@@ -67,7 +68,7 @@ def _goals(rows, n, seed):
     return rng.choice(free, size=min(n, free.size), replace=False).astype(np.uint32)
 
 
-@pytest.mark.parametrize("kernel", ["default", "blk", "wave", "block", "big"])
+@pytest.mark.parametrize("kernel", ["default", "mg", "blk", "wave", "block", "big"])
 @pytest.mark.parametrize("name", sorted(GRIDS))
 def test_bfs_kernels_bit_exact(kernel, name):
     rows = GRIDS[name]()
@@ -115,7 +116,7 @@ def test_bfs_blk_list_overflow(cap, wls):
     _check(rows, _goals(rows, 24, 3), TSW_BFS_KERNEL="blk", TSW_BFS_BLKCAP=cap, TSW_BFS_WLS=wls)
 
 
-@pytest.mark.parametrize("kernel", ["blk", "blk-pair", "wave", "big"])
+@pytest.mark.parametrize("kernel", ["mg", "blk", "blk-pair", "wave", "big"])
 def test_bfs_wave_unreachable_pockets(kernel):
     """Walled-off pockets stay 0xFFFF; goals inside a pocket see only the pocket."""
     a = np.zeros((40, 70), dtype=bool)
@@ -155,7 +156,7 @@ class _DevBuf:
         self.hip.hipFree(self.ptr)
 
 
-@pytest.mark.parametrize("kernel", ["blk", "blk-pair", "wave", "big"])
+@pytest.mark.parametrize("kernel", ["mg", "blk", "blk-pair", "wave", "big"])
 def test_bfs_den520d_full_size(kernel):
     """BASELINE configs[3] geometry: 256x257 cave, 1,000 distinct goals through the device-output
     entry point the bench times (16-B stores), every table bit-exact vs the oracle."""
@@ -174,7 +175,7 @@ def test_bfs_den520d_full_size(kernel):
         assert np.array_equal(got[k], ref), f"goal {g}: {np.count_nonzero(got[k] != ref)} cells differ"
 
 
-@pytest.mark.parametrize("kernel", ["blk", "wave", "big"])
+@pytest.mark.parametrize("kernel", ["mg", "blk", "wave", "big"])
 def test_bfs_symmetry_full_goal_set(kernel):
     """Size-independent property at full size: d_g(c) == d_c(g) for every pair of goals, over all
     free cells of a 96x97 cave used as goals (the table matrix restricted to goals is symmetric),
@@ -210,3 +211,11 @@ def test_bfs_den520d_10k_goals_as_benched():
     dig = table_digests(got)
     bad = np.flatnonzero(dig != ref["sha1_8"])
     assert bad.size == 0, f"{bad.size} of {goals.size} tables differ, first goal {goals[bad[0]]}"
+
+
+@pytest.mark.parametrize("name,n", [("comb70x20", 300), ("rand100x31", 1500), ("cave64", 2000), ("warehouse", 700)])
+def test_bfs_mg_many_groups(name, n):
+    """k_bfs_mg with many groups per launch: both parities, partial groups, groups dequeued by more
+    workgroups than CUs hold at once (scratch reuse across groups)."""
+    rows = GRIDS[name]()
+    _check(rows, _goals(rows, n, 21), TSW_BFS_KERNEL="mg")

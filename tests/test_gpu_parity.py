@@ -418,3 +418,29 @@ def test_mapd_workers_leave_when_idle(monkeypatch):
     st = _plan_vs_oracle(rows, starts, tasks, 150, diag=True)
     assert st["coop_workers"] > 0 and st["watchdog_fires"] == 0
     assert st["walker_launches"] >= 2, st["walker_launches"]  # the planner did give up on absent workers
+
+
+@pytest.mark.parametrize("case", range(4))
+@pytest.mark.parametrize("flags", [0, TSW_F_EXIT_MODE])
+def test_mapd_task_cells_checked_when_used(case, flags):
+    """Off-grid/blocked task cells fail the call only where the reference panics (pickup assigned,
+    tswap.rs:136; delivery looked up on reaching the pickup, :112); otherwise the plan is bit-exact."""
+    from test_oracle import _lazy_task_cases
+    from p2p_distributed_tswap_amd import TSW_EINVAL, TswapError
+
+    rows, starts, tasks, max_t, fails = _lazy_task_cases()[case]
+    og = OracleGraph(maps.rows_to_array(rows))
+    with Planner(rows, flags=flags) as p:
+        if fails:
+            with pytest.raises(TswapError) as ei:
+                p.plan_mapd_arrays(starts, tasks, max_t)
+            assert ei.value.code == TSW_EINVAL
+            # the context stays usable: a valid plan afterwards is still exact
+            ok = tasks[:2] if case == 1 else tasks[:0]
+            ref, _ = og.mapd(starts, ok, 50)
+            rec, _ = p.plan_mapd_arrays(starts, ok, 50)
+            assert np.array_equal(rec, ref)
+            return
+        ref, rgoal = og.mapd(starts, tasks, max_t, trace_goals=True)
+        rec, goal = p.plan_mapd_arrays(starts, tasks, max_t, trace_goals=True)
+    assert np.array_equal(goal, rgoal) and np.array_equal(rec, ref)
