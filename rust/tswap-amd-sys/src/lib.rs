@@ -4,9 +4,11 @@
 //! `tests/test_host.py::test_rust_crate_mirrors_header` checks it), plus a safe owner `Planner`
 //! whose methods take and return the reference's own shapes:
 //!
-//! * `Planner::tswap_mapd`  — `pub fn tswap_mapd(grid, initial_positions, tasks)`
-//!   (src/algorithm/tswap.rs:39-43): same arguments, same `Vec<Vec<(Point, AgentState)>>`;
-//!   the reference panics where this returns `Err` (tswap.rs:94,112,136).
+//! * `tswap_mapd` (free function) — the reference's exact signature and return type
+//!   (src/algorithm/tswap.rs:39-43) over the caller's own `Task` / `AgentState` through the
+//!   `TaskLike` / `FromAgentState` traits; panics where the reference panics.
+//! * `Planner::tswap_mapd`  — the same plan on a long-lived context, returning `Err` where the
+//!   reference panics (tswap.rs:94,112,136).
 //! * `Planner::step`        — the private `tswap_step(&mut agents, &nodes)` copy the centralized
 //!   manager calls from `plan_all_paths` (src/bin/centralized/manager.rs:101-144, :147-259).
 //! * `Planner::get_path_next` — `get_path(start, goal, nodes)` reduced to what its callers read:
@@ -175,6 +177,56 @@ impl AgentState {
     }
 }
 
+/// What the planner reads of the reference's `Task` (src/map/task_generator.rs:6-12): its two
+/// points (peer_id / task_id are never read, tswap.rs:106-139). The caller's crate adds
+/// `impl TaskLike for map::task_generator::Task` (two one-line methods) and passes `&[Task]`
+/// unchanged.
+pub trait TaskLike {
+    fn pickup(&self) -> Point;
+    fn delivery(&self) -> Point;
+}
+
+impl TaskLike for (Point, Point) {
+    fn pickup(&self) -> Point {
+        self.0
+    }
+    fn delivery(&self) -> Point {
+        self.1
+    }
+}
+
+/// Builds the caller's own `AgentState` (src/map/agent.rs:9-15) from this crate's, so the return
+/// type is exactly the reference's `Vec<Vec<(Point, AgentState)>>`. The caller's crate adds
+/// `impl FromAgentState for map::agent::AgentState` (a four-arm match).
+pub trait FromAgentState {
+    fn from_agent_state(s: AgentState) -> Self;
+}
+
+impl FromAgentState for AgentState {
+    fn from_agent_state(s: AgentState) -> Self {
+        s
+    }
+}
+
+/// Drop-in with the reference's exact signature, `pub fn tswap_mapd(grid: &[Vec<char>],
+/// initial_positions: Vec<Point>, tasks: &[Task]) -> Vec<Vec<(Point, AgentState)>>`
+/// (src/algorithm/tswap.rs:39-43): swap `use crate::algorithm::tswap::tswap_mapd` for
+/// `use tswap_amd_sys::tswap_mapd` and the call sites stay as they are. Like the reference it
+/// panics where the plan is invalid (an off-grid or blocked start, or a task cell looked up when
+/// assigned / reached, tswap.rs:94,112,136) and stops after timestep 2000 (:167). It builds a
+/// context per call, as the reference rebuilds its graph per call; keep a `Planner` instead to
+/// reuse tables across calls.
+pub fn tswap_mapd<T: TaskLike, S: FromAgentState>(grid: &[Vec<char>], initial_positions: Vec<Point>,
+                                                  tasks: &[T]) -> Vec<Vec<(Point, S)>> {
+    let mut planner = Planner::new(grid).unwrap_or_else(|e| panic!("{}", e));
+    planner
+        .tswap_mapd_tasks(initial_positions, tasks, 2000)
+        .unwrap_or_else(|e| panic!("{}", e))
+        .into_iter()
+        .map(|path| path.into_iter().map(|(p, s)| (p, S::from_agent_state(s))).collect())
+        .collect()
+}
+
 /// A failed call: the C error code and `tsw_last_error`'s message.
 #[derive(Clone, Debug)]
 pub struct TswapError {
@@ -278,13 +330,24 @@ impl Planner {
     /// `timestep > 2000` stop.
     pub fn tswap_mapd(&mut self, initial_positions: Vec<Point>, tasks: &[(Point, Point)], max_t: u32)
                       -> Result<Vec<Vec<(Point, AgentState)>>, TswapError> {
+        self.tswap_mapd_tasks(initial_positions, tasks, max_t)
+    }
+
+    /// As `tswap_mapd`, over any task type exposing the reference `Task`'s two points.
+    /// Coordinates past u32 saturate (such a point is off-grid either way).
+    pub fn tswap_mapd_tasks<T: TaskLike>(&mut self, initial_positions: Vec<Point>, tasks: &[T], max_t: u32)
+                                         -> Result<Vec<Vec<(Point, AgentState)>>, TswapError> {
+        let c32 = |v: usize| v.min(u32::MAX as usize) as u32;
         let starts: Vec<TswPoint> =
-            initial_positions.iter().map(|&(x, y)| TswPoint { x: x as u32, y: y as u32 }).collect();
+            initial_positions.iter().map(|&(x, y)| TswPoint { x: c32(x), y: c32(y) }).collect();
         let ts: Vec<TswTask> = tasks
             .iter()
-            .map(|&(p, d)| TswTask {
-                pickup: TswPoint { x: p.0 as u32, y: p.1 as u32 },
-                delivery: TswPoint { x: d.0 as u32, y: d.1 as u32 },
+            .map(|t| {
+                let (p, d) = (t.pickup(), t.delivery());
+                TswTask {
+                    pickup: TswPoint { x: c32(p.0), y: c32(p.1) },
+                    delivery: TswPoint { x: c32(d.0), y: c32(d.1) },
+                }
             })
             .collect();
         let n = starts.len();
