@@ -58,6 +58,11 @@ extern "C" {
 #define TSW_EOVERFLOW (-75)
 #define TSW_ENODEV (-19)
 
+/* Revision of this ABI: bumped whenever a struct or a signature changes, so a caller
+ * built against an older header can refuse to run. 3: tsw_opts grew to 24 bytes (watchdog_ms),
+ * tsw_next_hop_tables_device gained dev_dist; 4: tsw_abi_version, lazy task-cell checks. */
+#define TSW_ABI_VERSION 4
+
 /* AgentState discriminants in declaration order (src/map/agent.rs:9-15) */
 #define TSW_PICKING 0
 #define TSW_CARRYING 1
@@ -120,6 +125,8 @@ tsw_ctx *tsw_create(const uint8_t *cells, uint32_t w, uint32_t h, const tsw_opts
 void tsw_destroy(tsw_ctx *ctx);
 /* Message of the last failure on ctx (ctx may be NULL: last create failure). */
 const char *tsw_last_error(const tsw_ctx *ctx);
+/* TSW_ABI_VERSION the library was built with; compare it with the header's before tsw_create. */
+int tsw_abi_version(void);
 
 /* Replaces `tswap_mapd(grid, initial_positions, tasks)` (tswap.rs:39-172).
  * out: caller-allocated n*(max_t+1) records, agent-major:
@@ -187,7 +194,10 @@ int tsw_import_tables_device(tsw_ctx *ctx, const uint32_t *goals, uint32_t k,
 /* Next-hop codes of k goal tables (building them if needed), one byte per cell,
  * row-major: 0..3 = path[1] is the S,E,N,W neighbour (tswap.rs:62 order), 4 = stay
  * (unreachable goal, no closer neighbour), 0xFF = not resolved yet (lazy mode:
- * needs the exact A*). out: host buffer k*w*h. */
+ * needs the exact A*). out: host buffer k*w*h. A goal held without a distance table
+ * (u16 overflow, see the limits above) always comes back all 0xFF here, also with
+ * TSW_F_EAGER_NEXTHOP: its next hops are resolved per query (tsw_get_path_next, plans),
+ * never as a whole table; tsw_next_hop_tables_device returns TSW_EOVERFLOW for it. */
 int tsw_next_hop_tables(tsw_ctx *ctx, const uint32_t *goals, uint32_t k, uint8_t *out);
 
 /* Goal-sharded K3: the fully resolved next-hop codes of k goals into

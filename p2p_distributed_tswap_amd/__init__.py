@@ -35,6 +35,7 @@ LIB_PATH = os.path.join(_HERE, "libtswap_hip.so")
 DIAG_LIB_PATH = os.path.join(_HERE, "libtswap_hip_diag.so")
 
 TSW_OK, TSW_EINVAL, TSW_ENOMEM, TSW_EHIP, TSW_EOVERFLOW = 0, -22, -12, -5, -75
+TSW_ABI_VERSION = 4  # include/tswap.h
 TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP, TSW_F_EXIT_MODE = 1, 2, 4
 # TswapAction (bin/decentralized/agent.rs:321-326), include/tswap.h TSW_ACT_*
 TSW_ACT_MOVE, TSW_ACT_GOAL_SWAP, TSW_ACT_ROTATION, TSW_ACT_WAIT = 0, 1, 2, 3
@@ -116,6 +117,7 @@ EXPORTED_SYMBOLS = (
     "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables", "tsw_dist_tables_device",
     "tsw_import_tables_device", "tsw_next_hop_tables", "tsw_next_hop_tables_device", "tsw_import_next_hops_device",
     "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing", "tsw_probe_round_floors",
+    "tsw_abi_version",
 )
 
 _libs = {}
@@ -154,6 +156,11 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_reset_stats.argtypes = [vp]
     lib.tsw_set_timing.argtypes = [vp, ctypes.c_int]
     lib.tsw_probe_round_floors.argtypes = [vp, ctypes.c_uint32, P(ctypes.c_double)]
+    lib.tsw_abi_version.argtypes = []
+    lib.tsw_abi_version.restype = ctypes.c_int
+    if lib.tsw_abi_version() != TSW_ABI_VERSION:
+        raise TswapError(TSW_EINVAL, f"{path}: ABI {lib.tsw_abi_version()}, this binding mirrors {TSW_ABI_VERSION} "
+                                     "(rebuild with __graft_entry__.build())")
     for name in ("tsw_plan_mapd", "tsw_plan_mapd_trace", "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables",
                  "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_clear_tables", "tsw_next_hop_tables",
                  "tsw_next_hop_tables_device", "tsw_import_next_hops_device", "tsw_get_stats", "tsw_reset_stats",

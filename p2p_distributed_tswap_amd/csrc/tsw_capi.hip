@@ -533,8 +533,12 @@ int check_err(tsw_ctx* c) {
 // Run K3 over the queued queries until none are left (eager next hops).
 // K3 over nq queued queries (device array Q): LDS-heap kernel on small grids, with the
 // global-heap kernel for the few whose heap outgrows LDS; global-heap kernel otherwise.
+// res / lens (per-query answers, indexed by AstarQuery::out) only for queues the host filled itself
+// (tsw_get_path_next): queues written by k_plan reuse `out` for a diagnostic enqueue timestamp in
+// coop mode and are always run with res == lens == nullptr, writing codes into the tables.
 int run_astar(tsw_ctx* c, const AstarQuery* Q, uint32_t nq, bool to_tables, uint8_t* res, int32_t* lens) {
   if (nq == 0) return TSW_OK;
+  if ((res || lens) && to_tables) RET(TSW_EINVAL, "internal: per-query answers are not table writes");
   TRY(ensure_astar_scratch(c));
   Timer t(c, CAT_ASTAR);
   uint8_t* nh = to_tables ? c->d_nh : nullptr;
@@ -1270,7 +1274,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.epochs = c->d_epochs;
     W.heaps = c->d_heaps;
     W.ghcap = c->hcap;
-    const WorkerCfg wcfg = worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs, c->tun.dag_exit);
+    const WorkerCfg wcfg =
+        worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs, c->tun.dag_exit, lds);
     W.dag = wcfg.dag;
     // the test's heap scan gathers D from LDS (detour bytes) or from the u16 table in global memory:
     // every 16 / 64 pops (C3 worker busy -20 %, wh10k 400 steps 5.77 -> 5.42 s; profiles/r3/dag_exit_ab.txt)
@@ -1767,6 +1772,8 @@ void tsw_destroy(tsw_ctx* c) {
 }
 
 const char* tsw_last_error(const tsw_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
+
+int tsw_abi_version(void) { return TSW_ABI_VERSION; }
 
 int tsw_plan_mapd(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* tasks, uint32_t m,
                   uint32_t max_t, tsw_rec* out, uint32_t* out_T) {

@@ -708,7 +708,11 @@ hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const
 
 
 WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs,
-                        bool dag_exit) {
+                        bool dag_exit, size_t lds_cap) {
+  // the workers' LDS is the plan dispatch's per-workgroup request (the planner's, just under the
+  // CU's 160 KiB): every carve below must fit THAT, not the CU (C5's bitmap + heap
+  // came to 160 KiB, 2 KiB over the dispatch's request, and no worker fit — exit mode)
+  const size_t WAVE_LDS_MAX = std::min<size_t>(lds_cap, ::tsw::WAVE_LDS_MAX);
   const size_t fbb = (size_t)G.H * G.Ww * 4u;
   const uint32_t want = hcap_want ? std::min(hcap_want, WAVE_HCAP) : WAVE_HCAP;
   // m: g-score placement; fb: free bitmap in LDS. With LDS g-scores the DAG early exit stages the

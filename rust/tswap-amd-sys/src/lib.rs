@@ -33,6 +33,10 @@ pub const TSW_EHIP: c_int = -5;
 pub const TSW_EOVERFLOW: c_int = -75;
 pub const TSW_ENODEV: c_int = -19;
 
+/// ABI revision of include/tswap.h this crate mirrors; `Planner::new` refuses a library built
+/// against another one.
+pub const TSW_ABI_VERSION: c_int = 4;
+
 pub const TSW_PICKING: u8 = 0;
 pub const TSW_CARRYING: u8 = 1;
 pub const TSW_DELIVERED: u8 = 2;
@@ -125,6 +129,7 @@ extern "C" {
     pub fn tsw_create(cells: *const u8, w: u32, h: u32, opts: *const TswOpts) -> *mut TswCtx;
     pub fn tsw_destroy(ctx: *mut TswCtx);
     pub fn tsw_last_error(ctx: *const TswCtx) -> *const c_char;
+    pub fn tsw_abi_version() -> c_int;
     pub fn tsw_plan_mapd(ctx: *mut TswCtx, starts: *const TswPoint, n: u32, tasks: *const TswTask, m: u32,
                          max_t: u32, out: *mut TswRec, out_t: *mut u32) -> c_int;
     pub fn tsw_plan_mapd_trace(ctx: *mut TswCtx, starts: *const TswPoint, n: u32, tasks: *const TswTask, m: u32,
@@ -283,6 +288,13 @@ impl Planner {
         let w = if h > 0 { grid[0].len() } else { 0 };
         if grid.iter().any(|r| r.len() != w) {
             return Err(TswapError { code: TSW_EINVAL, message: "ragged grid rows".into() });
+        }
+        let abi = unsafe { tsw_abi_version() };
+        if abi != TSW_ABI_VERSION {
+            return Err(TswapError {
+                code: TSW_EINVAL,
+                message: format!("libtswap_hip ABI {} but this crate mirrors ABI {}", abi, TSW_ABI_VERSION),
+            });
         }
         let cells: Vec<u8> = grid.iter().flat_map(|r| r.iter().map(|&c| if c == '@' { b'@' } else { b'.' })).collect();
         let o = TswOpts {
