@@ -60,7 +60,8 @@ extern "C" {
 
 /* Revision of this ABI: bumped whenever a struct or a signature changes, so a caller
  * built against an older header can refuse to run. 3: tsw_opts grew to 24 bytes (watchdog_ms),
- * tsw_next_hop_tables_device gained dev_dist; 4: tsw_abi_version, lazy task-cell checks. */
+ * tsw_next_hop_tables_device gained dev_dist; 4: tsw_abi_version, lazy task-cell checks,
+ * tsw_plan_mapd_resolved / tsw_next_hop_codes. */
 #define TSW_ABI_VERSION 4
 
 /* AgentState discriminants in declaration order (src/map/agent.rs:9-15) */
@@ -147,6 +148,25 @@ int tsw_plan_mapd(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const tsw_t
 int tsw_plan_mapd_trace(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const tsw_task *tasks,
                         uint32_t m, uint32_t max_t, tsw_rec *out, uint32_t *goal_out,
                         uint32_t *out_T);
+
+/* Caller-resolved K3 (the per-step query batch sharded by goal owner, the
+ * answers gathered). tsw_plan_mapd_resolved plans like tsw_plan_mapd_trace, in exit mode (no K3
+ * workers in the plan dispatch), and hands every batch of (start, goal) cell pairs a step needs
+ * — plus the speculative pairs queued with it — to `resolve` instead of running the exact A*
+ * itself. resolve must fill code[i] with the next-hop code of get_path(start[i], goal[i]) (0..3
+ * = S,E,N,W neighbour, tswap.rs:62 order; 4 = stay), e.g. by sending each pair to the rank that
+ * owns its goal (tsw_next_hop_codes there) and gathering the codes, and return 0; anything else,
+ * or a code > 4, fails the call with TSW_EINVAL. The plan is bit-identical to tsw_plan_mapd's. */
+typedef int (*tsw_resolve_fn)(void *user, uint32_t k, const uint32_t *start, const uint32_t *goal, uint8_t *code);
+int tsw_plan_mapd_resolved(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const tsw_task *tasks,
+                           uint32_t m, uint32_t max_t, tsw_rec *out, uint32_t *goal_out, uint32_t *out_T,
+                           tsw_resolve_fn resolve, void *user);
+
+/* Next-hop codes of get_path(start[i], goal[i]) (tswap.rs:288-390) as tsw_plan_mapd_resolved's
+ * resolver returns them (0..3 S,E,N,W, 4 = stay), served from this context's table store: new
+ * goals get their K1 table, unresolved cells the exact A*, and both persist for later calls (a
+ * goal owner's shard of the next-hop cache). */
+int tsw_next_hop_codes(tsw_ctx *ctx, const uint32_t *start, const uint32_t *goal, uint32_t k, uint8_t *code);
 
 /* Replaces one `tswap_step(&mut agents, &nodes)` call (tswap.rs:174-286;
  * per-tick copy in bin/centralized/manager.rs:147-259 via plan_all_paths

@@ -117,8 +117,13 @@ EXPORTED_SYMBOLS = (
     "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables", "tsw_dist_tables_device",
     "tsw_import_tables_device", "tsw_next_hop_tables", "tsw_next_hop_tables_device", "tsw_import_next_hops_device",
     "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing", "tsw_probe_round_floors",
-    "tsw_abi_version",
+    "tsw_abi_version", "tsw_plan_mapd_resolved", "tsw_next_hop_codes",
 )
+
+# tsw_resolve_fn (include/tswap.h): int (*)(void *user, uint32_t k, const uint32_t *start,
+# const uint32_t *goal, uint8_t *code)
+_RESOLVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint8))
 
 _libs = {}
 
@@ -156,6 +161,11 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_reset_stats.argtypes = [vp]
     lib.tsw_set_timing.argtypes = [vp, ctypes.c_int]
     lib.tsw_probe_round_floors.argtypes = [vp, ctypes.c_uint32, P(ctypes.c_double)]
+    lib.tsw_plan_mapd_resolved.argtypes = [vp, P(_Point), u32, P(_Task), u32, u32, P(_Rec), P(u32), P(u32),
+                                           _RESOLVE_FN, vp]
+    lib.tsw_plan_mapd_resolved.restype = ctypes.c_int
+    lib.tsw_next_hop_codes.argtypes = [vp, P(u32), P(u32), u32, P(ctypes.c_uint8)]
+    lib.tsw_next_hop_codes.restype = ctypes.c_int
     lib.tsw_abi_version.argtypes = []
     lib.tsw_abi_version.restype = ctypes.c_int
     if lib.tsw_abi_version() != TSW_ABI_VERSION:
@@ -255,6 +265,57 @@ class Planner:
         t = T.value
         rec = out[:n, :t] & np.uint64(0xFFFFFFFFFF)
         return rec, (goals[:n, :t] if goals is not None else None)
+
+    def plan_mapd_resolved(self, starts_xy: np.ndarray, tasks_xyxy: np.ndarray, max_t: int, resolve,
+                           trace_goals: bool = False):
+        """tsw_plan_mapd_resolved: as plan_mapd_arrays, with every K3 batch answered by
+        resolve(start u32[k], goal u32[k]) -> u8[k] codes (e.g. sharding.ShardedK3.resolve)."""
+        starts = np.ascontiguousarray(starts_xy, dtype=np.uint32).reshape(-1, 2)
+        tasks = np.ascontiguousarray(tasks_xyxy, dtype=np.uint32).reshape(-1, 4)
+        n, m = starts.shape[0], tasks.shape[0]
+        stride = max_t + 1
+        out = np.zeros((max(n, 1), stride), dtype=np.uint64)
+        goals = np.zeros((max(n, 1), stride), dtype=np.uint32) if trace_goals else None
+        T = ctypes.c_uint32(0)
+        failure = []
+
+        def cb(user, k, sp, gp, cp):
+            try:
+                st = np.ctypeslib.as_array(sp, shape=(k,)).copy()
+                gl = np.ctypeslib.as_array(gp, shape=(k,)).copy()
+                codes = np.ascontiguousarray(resolve(st, gl), dtype=np.uint8)
+                if codes.shape != (k,):
+                    raise ValueError(f"resolver returned {codes.shape}, expected ({k},)")
+                ctypes.memmove(cp, codes.ctypes.data, k)
+                return 0
+            except BaseException as e:  # noqa: BLE001 — re-raised after the call returns
+                failure.append(e)
+                return 1
+
+        fn = _RESOLVE_FN(cb)
+        rc = self._lib.tsw_plan_mapd_resolved(
+            self._ctx, starts.ctypes.data_as(ctypes.POINTER(_Point)), n,
+            tasks.ctypes.data_as(ctypes.POINTER(_Task)), m, max_t, out.ctypes.data_as(ctypes.POINTER(_Rec)),
+            _u32p(goals) if goals is not None else None, ctypes.byref(T), fn, None)
+        if failure:
+            raise failure[0]
+        self._check(rc)
+        t = T.value
+        rec = out[:n, :t] & np.uint64(0xFFFFFFFFFF)
+        return rec, (goals[:n, :t] if goals is not None else None)
+
+    def next_hop_codes(self, start, goal) -> np.ndarray:
+        """tsw_next_hop_codes: u8 next-hop code of get_path(start[i], goal[i]) (0..3 S,E,N,W, 4 stay),
+        from this context's table store (K1 / exact A* for what it does not hold yet)."""
+        st = np.ascontiguousarray(start, dtype=np.uint32)
+        gl = np.ascontiguousarray(goal, dtype=np.uint32)
+        if st.shape != gl.shape:
+            raise TswapError(TSW_EINVAL, "start and goal must have the same length")
+        out = np.zeros(st.size, dtype=np.uint8)
+        if st.size:
+            self._check(self._lib.tsw_next_hop_codes(self._ctx, _u32p(st), _u32p(gl), st.size,
+                                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out
 
     def tswap_mapd(self, initial_positions: Sequence, tasks: Iterable, max_t: int = 2000):
         starts = np.array([[p[0], p[1]] for p in initial_positions], dtype=np.uint32).reshape(-1, 2)

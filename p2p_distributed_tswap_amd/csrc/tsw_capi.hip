@@ -219,6 +219,9 @@ struct tsw_ctx {
   uint32_t* d_flags = nullptr;
   uint64_t coop_aborts = 0;
   uint32_t watchdog_ms = 10000;  // tsw_opts.watchdog_ms
+  // tsw_plan_mapd_resolved: the caller resolves the exit batches (exit mode, lazy next hops)
+  tsw_resolve_fn resolver = nullptr;
+  void* resolver_user = nullptr;
 
   DevStatus* d_stat = nullptr;
   DevStatus* h_stat = nullptr;   // pinned, D2H
@@ -653,7 +656,7 @@ int resolve_all_unknown(tsw_ctx* c, const std::vector<uint32_t>& goals, const st
 }
 
 bool eager_policy(const tsw_ctx* c, size_t new_tables) {
-  if (c->flags & TSW_F_LAZY_NEXTHOP) return false;
+  if ((c->flags & TSW_F_LAZY_NEXTHOP) || c->resolver) return false;
   if (c->flags & TSW_F_EAGER_NEXTHOP) return true;
   return c->G.ncell <= 4096 && (uint64_t)new_tables * c->G.ncell <= (8ull << 20);
 }
@@ -1224,7 +1227,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.occ_lds = oc;
   P.tasks_lds = tk;
   // coop mode: lazy next hops only (eager tables have nothing left to resolve)
-  P.coop = (c->tun.coop && P.prefetch && c->d_cc && c->d_QS) ? 1u : 0u;
+  P.coop = (c->tun.coop && !c->resolver && P.prefetch && c->d_cc && c->d_QS) ? 1u : 0u;
   P.hflags = c->d_flags;  // watchdog words, both modes
   if (P.coop) {
     P.QS = c->d_QS;
@@ -1240,6 +1243,36 @@ int build_occ(tsw_ctx* c, uint32_t n) {
   HIPCHK(launch_occ(c->d_v, n, c->d_occ, c->d_cnt, c->G.ncell, c->d_dups, c->s));
   HIPCHK(hipMemcpyAsync(c->h_dups, c->d_dups, 4, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipStreamSynchronize(c->s));
+  return TSW_OK;
+}
+
+// The K3 pass of an exit-mode planner exit: the exact A* over the queue into the tables, or — with a
+// caller resolver (tsw_plan_mapd_resolved) — the queue's pairs handed to the caller and its codes
+// written into the tables.
+int resolve_queue(tsw_ctx* c, const AstarQuery* Q, uint32_t nq) {
+  if (!c->resolver) {
+    TRY(run_astar(c, Q, nq, true, nullptr, nullptr));
+    return check_err(c);
+  }
+  if (nq == 0) return TSW_OK;
+  std::vector<AstarQuery> q(nq);
+  HIPCHK(hipMemcpyAsync(q.data(), Q, (size_t)nq * sizeof(AstarQuery), hipMemcpyDeviceToHost, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  std::vector<uint32_t> st(nq), gl(nq);
+  for (uint32_t i = 0; i < nq; ++i) {
+    st[i] = q[i].v;
+    gl[i] = q[i].goal;
+  }
+  std::vector<uint8_t> codes(nq, NH_UNKNOWN);
+  if (c->resolver(c->resolver_user, nq, st.data(), gl.data(), codes.data()) != 0)
+    RET(TSW_EINVAL, "the caller's next-hop resolver failed");
+  for (uint32_t i = 0; i < nq; ++i)
+    if (codes[i] > NH_STAY) RET(TSW_EINVAL, "the caller's next-hop resolver returned a code > 4");
+  TRY(ensure_res(c, nq));
+  HIPCHK(hipMemcpyAsync(c->d_res, codes.data(), nq, hipMemcpyHostToDevice, c->s));
+  HIPCHK(launch_put_codes(Q, nq, c->d_res, c->d_nh, c->tstride, c->s));
+  HIPCHK(hipStreamSynchronize(c->s));
+  c->st.astar_queries += nq;
   return TSW_OK;
 }
 
@@ -1432,8 +1465,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       // is left PENDING for later calls (coop mode: the workers drained the needed queue)
       if (!coop && k.qcount > 0) {
         if (k.qcount > P.qcap) RET(TSW_EINVAL, "plan kernel queue overflow");
-        TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
-        TRY(check_err(c));
+        TRY(resolve_queue(c, c->d_Q, k.qcount));
       }
       return TSW_OK;
     }
@@ -1463,8 +1495,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     }
     if (k.status != PLAN_NEED_QUERIES || k.qcount == 0 || k.qcount > P.qcap)
       RET(TSW_EINVAL, "plan kernel stopped without resolvable next hops");
-    TRY(run_astar(c, c->d_Q, k.qcount, true, nullptr, nullptr));
-    TRY(check_err(c));
+    TRY(resolve_queue(c, c->d_Q, k.qcount));
   }
 }
 
@@ -1540,7 +1571,7 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   TRY(ensure_tables(c, goalset, true));
   TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
   c->qt_count = 0;
-  if (c->tun.coop && !eager_policy(c, 0)) {
+  if (c->tun.coop && !c->resolver && !eager_policy(c, 0)) {
     TRY(ensure_coop(c, n));
     if (c->tun.task_chains && m) {
       // every task's pickup -> delivery path, resolved hop by hop by the workers in the background
@@ -1785,6 +1816,69 @@ int tsw_plan_mapd_trace(tsw_ctx* c, const tsw_point* starts, uint32_t n, const t
                         uint32_t max_t, tsw_rec* out, uint32_t* goal_out, uint32_t* out_T) {
   if (!c) return TSW_EINVAL;
   return plan_impl(c, starts, n, tasks, m, max_t, out, goal_out, out_T);
+}
+
+int tsw_plan_mapd_resolved(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* tasks, uint32_t m,
+                           uint32_t max_t, tsw_rec* out, uint32_t* goal_out, uint32_t* out_T, tsw_resolve_fn resolve,
+                           void* user) {
+  if (!c) return TSW_EINVAL;
+  if (!resolve) RET(TSW_EINVAL, "null resolver");
+  c->resolver = resolve;
+  c->resolver_user = user;
+  const int rc = plan_impl(c, starts, n, tasks, m, max_t, out, goal_out, out_T);
+  c->resolver = nullptr;
+  c->resolver_user = nullptr;
+  return rc;
+}
+
+int next_hop_codes_impl(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, uint32_t k, uint8_t* code) {
+  for (uint32_t i = 0; i < k; ++i)
+    if (!cell_id_ok(c, start[i]) || !cell_id_ok(c, goal[i])) RET(TSW_EINVAL, "query cell off-grid or blocked");
+  std::vector<uint32_t> goals(goal, goal + k);
+  std::sort(goals.begin(), goals.end());
+  goals.erase(std::unique(goals.begin(), goals.end()), goals.end());
+  TRY(ensure_tables(c, goals, true));
+  std::vector<AstarQuery> q;
+  q.reserve(k);
+  for (uint32_t i = 0; i < k; ++i) {
+    if (start[i] == goal[i]) {
+      code[i] = NH_STAY;
+      continue;
+    }
+    q.push_back(AstarQuery{start[i], goal[i], c->h_goal_tab[goal[i]], i});
+  }
+  if (q.empty()) return TSW_OK;
+  const uint32_t nq = (uint32_t)q.size();
+  TRY(ensure_queue(c, nq));
+  TRY(ensure_res(c, nq));
+  std::vector<uint8_t> res(nq);
+  for (int pass = 0; pass < 2; ++pass) {
+    HIPCHK(hipMemcpyAsync(c->d_Q, q.data(), (size_t)nq * sizeof(AstarQuery), hipMemcpyHostToDevice, c->s));
+    HIPCHK(launch_gather_codes(c->d_Q, nq, c->d_nh, c->tstride, c->d_res, c->s));
+    HIPCHK(hipMemcpyAsync(res.data(), c->d_res, nq, hipMemcpyDeviceToHost, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));
+    std::vector<AstarQuery> miss;
+    for (uint32_t i = 0; i < nq; ++i)
+      if (res[i] > NH_STAY) miss.push_back(q[i]);
+    if (miss.empty()) break;
+    if (pass == 1) RET(TSW_EINVAL, "next hop left unresolved by K3");
+    // the exact A* into the tables (the store keeps them for later calls)
+    HIPCHK(hipMemcpyAsync(c->d_Q, miss.data(), miss.size() * sizeof(AstarQuery), hipMemcpyHostToDevice, c->s));
+    TRY(run_astar(c, c->d_Q, (uint32_t)miss.size(), true, nullptr, nullptr));
+    TRY(check_err(c));
+  }
+  for (uint32_t i = 0; i < nq; ++i) code[q[i].out] = res[i];
+  return TSW_OK;
+}
+
+int tsw_next_hop_codes(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, uint32_t k, uint8_t* code) {
+  if (!c) return TSW_EINVAL;
+  if (k == 0) return TSW_OK;
+  if (!start || !goal || !code) RET(TSW_EINVAL, "null argument");
+  TRY(set_device(c));
+  const int rc = reset_pending_after(c, next_hop_codes_impl(c, start, goal, k, code));
+  resolve_timing(c);
+  return rc;
 }
 
 int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {

@@ -695,6 +695,39 @@ hipError_t launch_reset_pending(uint8_t* nh, uint64_t nbytes, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Caller-resolved K3 (tsw_plan_mapd_resolved / tsw_next_hop_codes): codes of queued (start, goal) pairs
+// out of / into the next-hop store. Q[i].tab is the goal's table slot.
+__global__ void k_gather_codes(const AstarQuery* __restrict__ Q, uint32_t nq, const uint8_t* __restrict__ nh,
+                               uint64_t nstride, uint8_t* __restrict__ out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
+    const AstarQuery q = Q[i];
+    out[i] = q.tab < 0 ? NH_UNKNOWN : nh[(uint64_t)q.tab * nstride + q.v];
+  }
+}
+__global__ void k_put_codes(const AstarQuery* __restrict__ Q, uint32_t nq, const uint8_t* __restrict__ codes,
+                            uint8_t* __restrict__ nh, uint64_t nstride) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nq; i += gridDim.x * blockDim.x) {
+    const AstarQuery q = Q[i];
+    if (q.tab >= 0) nh[(uint64_t)q.tab * nstride + q.v] = codes[i];
+  }
+}
+
+hipError_t launch_gather_codes(const AstarQuery* Q, uint32_t nq, const uint8_t* nh, uint64_t nstride, uint8_t* out,
+                               hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>((nq + 255u) / 256u, 4096u);
+  hipLaunchKernelGGL(k_gather_codes, dim3(grid), dim3(256), 0, s, Q, nq, nh, nstride, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_put_codes(const AstarQuery* Q, uint32_t nq, const uint8_t* codes, uint8_t* nh, uint64_t nstride,
+                            hipStream_t s) {
+  if (nq == 0) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>((nq + 255u) / 256u, 4096u);
+  hipLaunchKernelGGL(k_put_codes, dim3(grid), dim3(256), 0, s, Q, nq, codes, nh, nstride);
+  return hipGetLastError();
+}
+
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
                                   uint32_t qcap, hipStream_t s) {

@@ -148,6 +148,12 @@ hipError_t launch_astar_wave(const DevGrid& G, const AstarQuery* Q, uint32_t nq,
                              AstarQuery* ovf, uint32_t* novf, uint32_t hcap /*0: default*/, bool global_gs,
                              hipStream_t s, uint32_t* qnext = nullptr, uint32_t diag = 0);
 
+// codes of queued (start, goal) pairs out of / into the next-hop store (caller-resolved K3)
+hipError_t launch_gather_codes(const AstarQuery* Q, uint32_t nq, const uint8_t* nh, uint64_t nstride, uint8_t* out,
+                               hipStream_t s);
+hipError_t launch_put_codes(const AstarQuery* Q, uint32_t nq, const uint8_t* codes, uint8_t* nh, uint64_t nstride,
+                            hipStream_t s);
+
 // NH_PENDING -> NH_UNKNOWN over nbytes of next-hop codes (error recovery)
 hipError_t launch_reset_pending(uint8_t* nh, uint64_t nbytes, hipStream_t s);
 

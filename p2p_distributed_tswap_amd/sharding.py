@@ -83,3 +83,94 @@ def build_and_allgather_codes(goals: np.ndarray, ncell: int, rank: int, world: i
     dist.all_gather_into_tensor(full_d.view(torch.uint8), local_d.view(torch.uint8))
     dist.all_gather_into_tensor(full_c, local_c)
     return full_d, full_c
+
+
+# ---- per-step K3 sharded by goal owner (as specified) -------------------------
+# Rank 0 plans (tsw_plan_mapd_resolved: exit mode, the planner stops whenever a step needs next hops it
+# does not have). Each stop's batch of (start, goal) pairs is broadcast; rank r answers the pairs whose
+# goal it owns (goal % world == r) from its own table store (tsw_next_hop_codes: K1 for its new goals,
+# the exact A* for unresolved cells, both kept for later stops), and one all-reduce(MIN) over the u8
+# codes (non-owners contribute 0xFF) gathers the answers: <= 4n + 4096 bytes per stop. Every rank holds
+# only its goals' tables and A* state. The planner's own step stays sequential on rank 0 (§8e row 3).
+
+def goal_owner(goal: np.ndarray, world: int) -> np.ndarray:
+    return (np.asarray(goal, dtype=np.int64) % world).astype(np.int64)
+
+
+def _codes_for_rank(start: np.ndarray, goal: np.ndarray, rank: int, world: int,
+                    codes_fn: Callable[[np.ndarray, np.ndarray], np.ndarray]) -> np.ndarray:
+    """u8 codes of the pairs this rank owns, 0xFF elsewhere (the all-reduce MIN fills the rest)."""
+    out = np.full(start.size, 0xFF, dtype=np.uint8)
+    mine = np.flatnonzero(goal_owner(goal, world) == rank)
+    if mine.size:
+        out[mine] = codes_fn(np.ascontiguousarray(start[mine]), np.ascontiguousarray(goal[mine]))
+    return out
+
+
+class ShardedK3:
+    """The collective half of the protocol. `codes_fn(start, goal) -> u8 codes` answers this rank's
+    pairs (Planner.next_hop_codes on MI355X; the oracle in the CPU gloo tests)."""
+
+    def __init__(self, rank: int, world: int, dist, device, codes_fn):
+        self.rank, self.world, self.dist, self.device, self.codes_fn = rank, world, dist, device, codes_fn
+        self.stops = 0
+        self.pairs = 0
+
+    def _bcast(self, arr: np.ndarray, dtype, n: int):
+        import torch
+
+        t = torch.zeros(n, dtype=dtype, device=self.device)
+        if self.rank == 0:
+            t.copy_(torch.from_numpy(arr))
+        self.dist.broadcast(t, src=0)
+        return t.cpu().numpy()
+
+    def _exchange(self, start: np.ndarray, goal: np.ndarray) -> np.ndarray:
+        import torch
+
+        k = int(self._bcast(np.array([start.size if self.rank == 0 else 0], np.int64), torch.int64, 1)[0])
+        if k < 0:
+            return None
+        pairs = np.concatenate([start, goal]).astype(np.int32) if self.rank == 0 else None
+        pairs = self._bcast(pairs, torch.int32, 2 * k).astype(np.uint32)
+        st, gl = pairs[:k], pairs[k:]
+        mine = _codes_for_rank(st, gl, self.rank, self.world, self.codes_fn)
+        # u8 codes ride in an int32 tensor (MIN over ranks: the owner's code, others 0xFF)
+        t = torch.from_numpy(mine.astype(np.int32)).to(self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+        self.stops += 1
+        self.pairs += k
+        return t.cpu().numpy().astype(np.uint8)
+
+    def resolve(self, start: np.ndarray, goal: np.ndarray) -> np.ndarray:
+        """Rank 0's resolver (one planner stop)."""
+        codes = self._exchange(start, goal)
+        if np.any(codes > 4):
+            raise RuntimeError("a next hop was answered by no rank")
+        return codes
+
+    def serve(self) -> None:
+        """Ranks > 0: answer stops until rank 0's plan ends (finish())."""
+        while self._exchange(np.zeros(0, np.uint32), np.zeros(0, np.uint32)) is not None:
+            pass
+
+    def finish(self) -> None:
+        """Rank 0: release the serving ranks."""
+        import torch
+
+        self._bcast(np.array([-1], np.int64), torch.int64, 1)
+
+
+def plan_sharded_k3(rank: int, world: int, dist, device, codes_fn, plan_fn=None):
+    """All ranks call this. Rank 0 runs plan_fn(resolver) (e.g. lambda r: planner.plan_mapd_resolved(
+    starts, tasks, 2000, r, trace_goals=True)) and returns its result; other ranks serve until it ends.
+    Returns (result or None, ShardedK3 with per-rank stop / pair counts)."""
+    sk = ShardedK3(rank, world, dist, device, codes_fn)
+    if rank == 0:
+        try:
+            res = plan_fn(sk.resolve)
+        finally:
+            sk.finish()
+        return res, sk
+    sk.serve()
+    return None, sk

@@ -21,7 +21,7 @@
 //! `table_budget_bytes`).
 
 use std::ffi::CStr;
-use std::os::raw::{c_char, c_int};
+use std::os::raw::{c_char, c_int, c_void};
 
 // ---------------------------------------------------------------------------------------------
 // raw C ABI (include/tswap.h)
@@ -52,6 +52,11 @@ pub const TSW_ACT_MOVE: u32 = 0;
 pub const TSW_ACT_GOAL_SWAP: u32 = 1;
 pub const TSW_ACT_ROTATION: u32 = 2;
 pub const TSW_ACT_WAIT: u32 = 3;
+
+/// `tsw_resolve_fn`: the caller's K3 for `tsw_plan_mapd_resolved` — fill `code[i]` (0..3 S,E,N,W,
+/// 4 stay) for get_path(start[i], goal[i]) and return 0 (e.g. send each pair to its goal's owner).
+pub type TswResolveFn =
+    Option<unsafe extern "C" fn(user: *mut c_void, k: u32, start: *const u32, goal: *const u32, code: *mut u8) -> c_int>;
 
 #[repr(C)]
 pub struct TswCtx {
@@ -129,6 +134,10 @@ extern "C" {
     pub fn tsw_create(cells: *const u8, w: u32, h: u32, opts: *const TswOpts) -> *mut TswCtx;
     pub fn tsw_destroy(ctx: *mut TswCtx);
     pub fn tsw_last_error(ctx: *const TswCtx) -> *const c_char;
+    pub fn tsw_plan_mapd_resolved(ctx: *mut TswCtx, starts: *const TswPoint, n: u32, tasks: *const TswTask, m: u32,
+                                  max_t: u32, out: *mut TswRec, goal_out: *mut u32, out_t: *mut u32,
+                                  resolve: TswResolveFn, user: *mut c_void) -> c_int;
+    pub fn tsw_next_hop_codes(ctx: *mut TswCtx, start: *const u32, goal: *const u32, k: u32, code: *mut u8) -> c_int;
     pub fn tsw_abi_version() -> c_int;
     pub fn tsw_plan_mapd(ctx: *mut TswCtx, starts: *const TswPoint, n: u32, tasks: *const TswTask, m: u32,
                          max_t: u32, out: *mut TswRec, out_t: *mut u32) -> c_int;

@@ -80,3 +80,67 @@ def test_sharded_next_hops_then_plan(name, n, m, seed):
         st = p.stats()
     assert st["bfs_goals"] == 0 and st["astar_queries"] == 0  # no K1, no K3 on the planning GPU
     assert np.array_equal(goal, rgoal) and np.array_equal(rec, ref)
+
+
+@pytest.mark.parametrize("name,n,m,seed,world,max_t", [
+    ("warehouse", 300, 900, 5, 2, 2000),
+    ("warehouse", 1000, 3000, 0x170084, 3, 400),
+    ("rand32", 200, 600, 0x3232, 2, 2000),
+])
+def test_plan_with_k3_sharded_by_goal_owner(name, n, m, seed, world, max_t):
+    """SURVEY §8e row 2 as specified, on one device: the planner's every K3 batch goes to the
+    "rank" (its own context) owning each pair's goal (goal % world), answered by
+    tsw_next_hop_codes from that rank's table store, and gathered (sharding._codes_for_rank + MIN,
+    exactly what ShardedK3 does over RCCL). The plan equals the oracle's and the replica plan."""
+    from test_gpu_parity import _grid
+
+    rows = _grid(name)
+    starts, tasks = maps.make_instance(rows, n, m, seed)
+    og = OracleGraph(maps.rows_to_array(rows))
+    ref, rgoal = og.mapd(starts, tasks, max_t, trace_goals=True)
+    owners = [Planner(rows) for _ in range(world)]
+    calls = []
+
+    def resolve(st, gl):
+        calls.append(st.size)
+        parts = [sharding._codes_for_rank(st, gl, r, world, owners[r].next_hop_codes) for r in range(world)]
+        return np.minimum.reduce(parts)
+
+    try:
+        with Planner(rows) as p:
+            rec, goal = p.plan_mapd_resolved(starts, tasks, max_t, resolve, trace_goals=True)
+            st = p.stats()
+        assert st["bfs_goals"] > 0 and st["astar_launches"] == 0  # the planner ran no K3 itself
+        owned = [o.stats()["bfs_goals"] for o in owners]
+    finally:
+        for o in owners:
+            o.close()
+    assert calls and sum(owned) > 0 and min(owned) > 0  # every owner built its own goals' tables
+    if not np.array_equal(goal, rgoal):
+        t = int(np.argmax((goal != rgoal).any(axis=0)))
+        pytest.fail(f"goal divergence first at t={t}")
+    assert np.array_equal(rec, ref)
+
+
+def test_next_hop_codes_match_oracle():
+    """tsw_next_hop_codes (a goal owner's answers) == get_path(start, goal)[1] of the oracle, on
+    random pairs, twice (the second call is served from the store)."""
+    from test_gpu_parity import _grid
+
+    rows = _grid("warehouse")
+    cells = maps.rows_to_array(rows)
+    w = cells.shape[1]
+    og = OracleGraph(cells)
+    free = np.flatnonzero(cells.reshape(-1) != ord("@")).astype(np.uint32)
+    rng = np.random.default_rng(7)
+    st = rng.choice(free, 600).astype(np.uint32)
+    gl = rng.choice(free[:200], 600).astype(np.uint32)
+    st[:5] = gl[:5]  # start == goal: code 4
+    want = np.empty(st.size, np.uint8)
+    for i, (s, g) in enumerate(zip(st.tolist(), gl.tolist())):
+        nxt, _, _ = og.get_path_next(s, g)
+        d = nxt - s
+        want[i] = 4 if nxt == s else 0 if d == w else 1 if d == 1 else 2 if d == -w else 3
+    with Planner(rows) as p:
+        assert np.array_equal(p.next_hop_codes(st, gl), want)
+        assert np.array_equal(p.next_hop_codes(st, gl), want)
