@@ -93,8 +93,14 @@ __global__ void __launch_bounds__(1024) k_bfs_mg(MgBfsArgs A) {
   uint32_t* WL = A.wl + (uint64_t)blockIdx.x * A.wlw;
   uint16_t* AN = A.anch + (uint64_t)blockIdx.x * A.nrs * MG_G;
   const uint32_t vwords = mg_vbytes(W, H) / 4u;
+  // lane roles in a BFS task: half hf (block A / B of the task), cell i of the block's 32 cells of one
+  // parity (row r); mark lanes 0-9: direction dir (self, N, S, W, E) of block A (0-4) / B (5-9)
+  const uint32_t wvu = __builtin_amdgcn_readfirstlane(wv);
+  const uint32_t hf = lane >> 5, i = lane & 31u, r = i >> 2;
+  const uint32_t dir = lane < 5u ? lane : (lane < 10u ? lane - 5u : 0u);
+  const uint32_t toff = dir == 0u ? 0u : dir == 1u ? 0u - Bp : dir == 2u ? Bp : dir == 3u ? 0xFFFFFFFFu : 1u;
   const uint32_t Ww = (W + 31u) >> 5, nwords = H * Ww;
-  uint64_t t_bfs = 0, t_dec = 0, n_lvl = 0;
+  uint64_t t_bfs = 0, t_dec = 0, n_lvl = 0, n_blk = 0, t_list = 0, t_task = 0;
 
   for (;;) {
     __syncthreads();  // the previous group's decode is done with V before it is cleared
@@ -140,6 +146,7 @@ __global__ void __launch_bounds__(1024) k_bfs_mg(MgBfsArgs A) {
       const uint32_t* CBc = CB + (L % 3u) * nwc;
       uint32_t* CBn = CB + ((L + 1u) % 3u) * nwc;
       uint32_t* CBo = CB + ((L + 2u) % 3u) * nwc;  // read at level L-1: free to clear now
+      const uint64_t tl0 = A.prof ? clk() : 0ull;
       if (wv == 0) {
         uint32_t n = 0;
         for (uint32_t base = 0; base < nwc; base += 64u) {
@@ -164,32 +171,41 @@ __global__ void __launch_bounds__(1024) k_bfs_mg(MgBfsArgs A) {
         for (uint32_t t = tid - 64u; t < nwc; t += bd - 64u) CBo[t] = 0u;
       }
       __syncthreads();
-      const uint32_t n = s_n;
+      const uint32_t n = __builtin_amdgcn_readfirstlane(s_n);
+      const uint64_t tl1 = A.prof ? clk() : 0ull;
+      t_list += tl1 - tl0;
+      n_blk += n;
       if (n == 0u) break;
       if (L >= 0xFFFFu) {  // cannot happen with <= 65535 free cells (checked on the host)
         if (tid == 0) atomicOr(A.err, ERR_DIST_OVERFLOW);
         break;
       }
+      // per-lane constants of this level's parity: the lane's cell inside its block (row r, column
+      // col of parity P), its V offset, and its mark target (lanes 0-4: block A's self, N, S, W, E;
+      // lanes 5-9: block B's)
       const uint32_t P = (gpar + L) & 1u;
-      const uint32_t hf = lane >> 5, i = lane & 31u, r = i >> 2, col = 2u * (i & 3u) + ((r + P) & 1u);
-      const uint32_t bitc = r * 8u + col;
+      const uint32_t col = 2u * (i & 3u) + ((r + P) & 1u);
+      const uint32_t bitc = r * 8u + col, loff = r * Wp + col;
       const uint32_t mW = P ? 0x10101010u : 0x01010101u, mE = P ? 0x08080808u : 0x80808080u;
-      for (uint32_t t = wv; 2u * t < n; t += nwv) {
+      const uint32_t mmask = dir == 0u ? 0xFFFFFFFFu : dir == 1u ? 0xFu : dir == 2u ? 0xF0000000u : dir == 3u ? mW : mE;
+      for (uint32_t t = wvu; 2u * t < n; t += nwv) {
         const uint32_t e = 2u * t + hf;
         const uint32_t p = e < n ? (uint32_t)LIST[e] : 0u;  // block 0 is a guard (FR = 0)
-        const uint32_t by = p / Bp, bx = p - by * Bp;
+        const uint32_t by = __umulhi(p, A.bp_magic), bx = p - by * Bp;  // p / Bp, p % Bp
         const uint64_t fr = FR[p];
         const bool fre = (fr >> bitc) & 1ull;  // guard blocks and off-grid cells are not free
-        const uint32_t x = 8u * bx + col, y = 8u * by + r - 8u;  // by >= 1 for every free cell
-        const uint32_t a = fre ? (y + 1u) * Wp + x + 1u : Wp + 1u;
-        const uint32_t vc = V[a], vw = V[a - 1u], ve = V[a + 1u], vn = V[a - Wp], vs = V[a + Wp];
-        const uint32_t nw = fre ? ((vw | ve | vn | vs) & ~vc) & 0xFFFFu : 0u;
-        if (nw) {
-          V[a] = (uint16_t)(vc | nw);
-          const uint32_t cell = y * W + x;
-          const uint32_t wl = nw & vw;
-          if (wl) wl_or(WL + (cell >> 1), wl << ((cell & 1u) * 16u));
-          // run start: record the level for every new goal bit
+        // V index of the lane's cell; other lanes use the guard word V[Wp] (west of cell (0, 0), always
+        // 0: reads see no goal, the store below rewrites 0) — the store is then branch-free
+        const uint32_t a = fre ? (8u * by - 7u) * Wp + 8u * bx + 1u + loff : Wp;
+        const uint32_t vn = V[a - Wp], vw = V[a - 1u], vc = V[a], ve = V[a + 1u], vs = V[a + Wp];
+        const uint32_t nw = fre ? ((vn | vw | ve | vs) & ~vc) & 0xFFFFu : 0u;  // the guard word stays 0
+        V[a] = (uint16_t)(vc | nw);
+        const uint32_t wl = nw & vw;
+        if (wl) {
+          const uint32_t cell = (8u * by - 8u + r) * W + 8u * bx + col;
+          wl_or(WL + (cell >> 1), wl << ((cell & 1u) * 16u));
+        }
+        if (nw) {  // a run start records the level of every new goal bit
           const uint64_t rsm = rs_mask(FR, p, bx);
           if ((rsm >> bitc) & 1ull) {
             uint16_t* an = AN + (AB[p] + (uint32_t)__popcll(rsm & ((1ull << bitc) - 1ull))) * MG_G;
@@ -202,22 +218,15 @@ __global__ void __launch_bounds__(1024) k_bfs_mg(MgBfsArgs A) {
         }
         // exact marks for level L+1: the block itself, and a neighbour across an edge with new cells
         const uint64_t m = __ballot(nw != 0u);
-        const uint32_t mh = (uint32_t)(m >> (32u * (lane >= 5u ? 1u : 0u)));
-        const uint32_t ph = (uint32_t)__shfl(p, lane >= 5u ? 32 : 0);
-        const uint32_t dir = lane >= 5u ? lane - 5u : lane;
-        if (lane < 10u && (lane < 5u || 2u * t + 1u < n)) {
-          bool want;
-          uint32_t tg;
-          switch (dir) {
-            case 0: want = mh != 0u; tg = ph; break;
-            case 1: want = (mh & 0xFu) != 0u; tg = ph - Bp; break;
-            case 2: want = (mh & 0xF0000000u) != 0u; tg = ph + Bp; break;
-            case 3: want = (mh & mW) != 0u; tg = ph - 1u; break;
-            default: want = (mh & mE) != 0u; tg = ph + 1u; break;
-          }
-          if (want) atomicOr(&CBn[tg >> 5], 1u << (tg & 31u));
+        const uint32_t pA = __builtin_amdgcn_readlane(p, 0), pB = __builtin_amdgcn_readlane(p, 32);
+        const uint32_t mh = lane < 5u ? (uint32_t)m : (uint32_t)(m >> 32);
+        const bool want = lane < 10u && (mh & mmask) != 0u && (lane < 5u || 2u * t + 1u < n);
+        if (want) {
+          const uint32_t tg = (lane < 5u ? pA : pB) + toff;
+          atomicOr(&CBn[tg >> 5], 1u << (tg & 31u));
         }
       }
+      if (A.prof) t_task += clk() - tl1;
       __syncthreads();
     }
     n_lvl += L;
@@ -229,52 +238,73 @@ __global__ void __launch_bounds__(1024) k_bfs_mg(MgBfsArgs A) {
     // this CU's L1 may hold WL / anchor lines of the previous group (the atomics and the run-start
     // stores went to L2): invalidate before reading them
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const uint32_t gng = s_ng;
-    for (uint32_t t = wv; 2u * t < nwords; t += nwv) {
-      const uint32_t q = 2u * t + (lane >> 5), l = lane & 31u;
+    const uint32_t gng = __builtin_amdgcn_readfirstlane(s_ng);
+    uint32_t gslot[MG_G];
+#pragma unroll
+    for (uint32_t k = 0; k < MG_G; ++k) gslot[k] = __builtin_amdgcn_readfirstlane(s_gslot[k < gng ? k : 0u]);
+    // one task = two consecutive 32-cell row words (lanes 0-31 / 32-63); the next task's loads are
+    // issued before the current one is decoded (global latency off the per-task chain)
+    struct Dw {
+      uint32_t v, w, cell, rs;
+      bool valid;
+      uint4 a0, a1;
+    };
+    const uint32_t l = lane & 31u;
+    auto fetch = [&](uint32_t t, Dw& o) {
+      const uint32_t q = 2u * t + (lane >> 5);
       const uint32_t y = q / Ww, x = 32u * (q - y * Ww) + l;
-      const bool valid = q < nwords && x < W;
-      const uint32_t cell = y * W + x;
-      uint32_t v = 0u, w = 0u;
+      o.valid = q < nwords && x < W;
+      o.cell = y * W + x;
+      o.v = 0u;
+      o.w = 0u;
+      o.rs = 0u;
+      o.a0 = o.a1 = make_uint4(0, 0, 0, 0);
       bool fre = false;
-      uint32_t p = 0, bit = 0, bx = 0;
-      if (valid) {
-        v = V[(y + 1u) * Wp + x + 1u];
-        bx = x >> 3;
-        p = ((y >> 3) + 1u) * Bp + bx;
+      uint32_t p = 0, bit = 0;
+      if (o.valid) {
+        o.v = V[(y + 1u) * Wp + x + 1u];
+        p = ((y >> 3) + 1u) * Bp + (x >> 3);
         bit = ((y & 7u) << 3) | (x & 7u);
         fre = (FR[p] >> bit) & 1ull;
-        if (v) w = (WL[cell >> 1] >> ((cell & 1u) * 16u)) & 0xFFFFu;
       }
       // run start of this lane's cell inside its 32-cell word (x % 32 == 0 or west blocked)
       const uint64_t fm = __ballot(fre);
       const uint32_t fh = (uint32_t)(fm >> (lane & 32u));
       const uint32_t rsw = fh & ~(fh << 1);
-      const uint32_t upto = l == 31u ? 0xFFFFFFFFu : (2u << l) - 1u;
-      const uint32_t below = rsw & upto;
-      const uint32_t rs = below ? 31u - (uint32_t)__builtin_clz(below) : 0u;
-      const uint32_t mrun = upto & ~((2u << rs) - 1u);  // bits (rs, l]
-      uint4 a0 = make_uint4(0, 0, 0, 0), a1 = make_uint4(0, 0, 0, 0);
-      if (v) {
-        const uint32_t xr = x - l + rs, bxr = xr >> 3, pr = ((y >> 3) + 1u) * Bp + bxr;
+      const uint32_t below = rsw & (l == 31u ? 0xFFFFFFFFu : (2u << l) - 1u);
+      o.rs = below ? 31u - (uint32_t)__builtin_clz(below) : 0u;
+      if (o.v) {
+        o.w = WL[o.cell >> 1];
+        const uint32_t xr = x - l + o.rs, bxr = xr >> 3, pr = ((y >> 3) + 1u) * Bp + bxr;
         const uint32_t bitr = ((y & 7u) << 3) | (xr & 7u);
         const uint64_t rsm = rs_mask(FR, pr, bxr);
         const uint32_t ai = AB[pr] + (uint32_t)__popcll(rsm & ((1ull << bitr) - 1ull));
         const uint4* ap = reinterpret_cast<const uint4*>(AN + (uint64_t)ai * MG_G);
-        a0 = ap[0];
-        a1 = ap[1];
+        o.a0 = ap[0];
+        o.a1 = ap[1];
       }
-      const uint32_t an[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const int32_t base = -(int32_t)(l - rs);
+    };
+    const uint32_t ntask = (nwords + 1u) / 2u;
+    Dw cur, nxt;
+    if (wvu < ntask) fetch(wvu, cur);
+    for (uint32_t t = wvu; t < ntask; t += nwv) {
+      if (t + nwv < ntask) fetch(t + nwv, nxt);
+      const uint32_t w = (cur.w >> ((cur.cell & 1u) * 16u)) & 0xFFFFu;
+      const uint32_t upto = l == 31u ? 0xFFFFFFFFu : (2u << l) - 1u;
+      const uint32_t mrun = upto & ~((2u << cur.rs) - 1u);  // bits (rs, l]
+      const uint32_t an[8] = {cur.a0.x, cur.a0.y, cur.a0.z, cur.a0.w, cur.a1.x, cur.a1.y, cur.a1.z, cur.a1.w};
+      const int32_t base = -(int32_t)(l - cur.rs);
 #pragma unroll
-      for (uint32_t k = 0; k < MG_G; ++k) {  // unrolled: an[] stays in registers
-        if (k >= gng) break;
-        const uint64_t wk = __ballot((w >> k) & 1u);
-        const uint32_t pc = (uint32_t)__popc((uint32_t)(wk >> (lane & 32u)) & mrun);
-        const uint32_t ak = (an[k >> 1] >> ((k & 1u) * 16u)) & 0xFFFFu;
-        const uint32_t d = (uint32_t)((int32_t)(ak + 2u * pc) + base) & 0xFFFFu;
-        if (valid) A.dist[(uint64_t)s_gslot[k] * A.dstride + cell] = (uint16_t)(((v >> k) & 1u) ? d : 0xFFFFu);
+      for (uint32_t k = 0; k < MG_G; ++k) {  // unrolled: an[] and gslot[] stay in registers
+        if (k < gng) {
+          const uint64_t wk = __ballot((w >> k) & 1u);
+          const uint32_t pc = (uint32_t)__popc((uint32_t)(wk >> (lane & 32u)) & mrun);
+          const uint32_t ak = (an[k >> 1] >> ((k & 1u) * 16u)) & 0xFFFFu;
+          const uint32_t d = (uint32_t)((int32_t)(ak + 2u * pc) + base) & 0xFFFFu;
+          if (cur.valid) A.dist[(uint64_t)gslot[k] * A.dstride + cur.cell] = (uint16_t)(((cur.v >> k) & 1u) ? d : 0xFFFFu);
+        }
       }
+      cur = nxt;
     }
     if (A.prof) {
       t_bfs += t1 - t0;
@@ -285,6 +315,11 @@ __global__ void __launch_bounds__(1024) k_bfs_mg(MgBfsArgs A) {
     atomicAdd((unsigned long long*)&A.prof[0], (unsigned long long)t_bfs);
     atomicAdd((unsigned long long*)&A.prof[1], (unsigned long long)t_dec);
     atomicAdd((unsigned long long*)&A.prof[2], (unsigned long long)n_lvl);
+    atomicAdd((unsigned long long*)&A.prof[3], (unsigned long long)n_blk);
+  }
+  if (A.prof && lane == 0) {  // per wave: list build + barrier, own task loop (summed over waves)
+    atomicAdd((unsigned long long*)&A.prof[4], (unsigned long long)t_list);
+    atomicAdd((unsigned long long*)&A.prof[5], (unsigned long long)t_task);
   }
 }
 

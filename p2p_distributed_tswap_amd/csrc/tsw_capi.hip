@@ -393,13 +393,14 @@ int ensure_tmp(tsw_ctx* c, size_t k) {
 // wave of goals is the short ones (LPT scheduling) instead of a few long ones running on an
 // otherwise idle chip. Output positions are carried in `slots`. TSW_BFS_ORDER=0 keeps the
 // caller's order (A/B).
-// k_bfs_mg serves this launch: its LDS layout fits, levels fit u16 (<= 65535 free cells), and the
-// batch is large enough to fill groups (mode 5 forces it whenever it fits)
+// k_bfs_mg serves this launch: selected explicitly (TSW_BFS_KERNEL=mg, diagnostic build — measured
+// 5.5 ms vs k_bfs_blk's 2.7 ms on den520d's 10k goals), its LDS layout fits and the
+// levels fit u16 (<= 65535 free cells)
 bool mg_selected(const tsw_ctx* c, size_t k) {
-  if (c->tun.bfs_mode != 0u && c->tun.bfs_mode != 5u) return false;
+  (void)k;
+  if (c->tun.bfs_mode != 5u) return false;
   if (c->nfree > 0xFFFFu || c->nbp > 0xFFFFu || c->max_lds <= 0) return false;
-  if (bfs_mg_lds_bytes(c->G.W, c->G.H, c->nbp) > (size_t)c->max_lds) return false;
-  return c->tun.bfs_mode == 5u || k >= 64u;
+  return bfs_mg_lds_bytes(c->G.W, c->G.H, c->nbp) <= (size_t)c->max_lds;
 }
 
 uint32_t morton2(uint32_t x, uint32_t y) {
@@ -686,17 +687,19 @@ int ensure_wave_scratch(tsw_ctx* c, uint64_t want, size_t words, size_t lwords) 
 
 unsigned long long* bfs_prof_buf(tsw_ctx* c) {
   if (!c->tun.bfs_prof) return nullptr;
-  if (!c->d_bprof && hipMalloc(&c->d_bprof, 4 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(c->d_bprof, 0, 4 * sizeof(unsigned long long), c->s) != hipSuccess) return nullptr;
+  if (!c->d_bprof && hipMalloc(&c->d_bprof, 8 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(c->d_bprof, 0, 8 * sizeof(unsigned long long), c->s) != hipSuccess) return nullptr;
   return c->d_bprof;
 }
 
 int bfs_prof_print(tsw_ctx* c, const char* name, uint32_t k) {
-  unsigned long long h[4] = {0, 0, 0, 0};
+  unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   HIPCHK(hipMemcpyAsync(h, c->d_bprof, sizeof h, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipStreamSynchronize(c->s));
-  fprintf(stderr, "[%s] goals %u  bfs %.0f cyc/goal  decode %.0f cyc/goal  levels %.1f/goal  chunks %.1f/goal\n",
-          name, k, (double)h[0] / k, (double)h[1] / k, (double)h[2] / k, (double)h[3] / k);
+  fprintf(stderr, "[%s] goals %u  bfs %.0f cyc/goal  decode %.0f cyc/goal  levels %.1f/goal  chunks %.1f/goal"
+          "  (mg: wave-cycles list+barrier %.0f, tasks %.0f per goal)\n",
+          name, k, (double)h[0] / k, (double)h[1] / k, (double)h[2] / k, (double)h[3] / k, (double)h[4] / k,
+          (double)h[5] / k);
   return TSW_OK;
 }
 
@@ -737,6 +740,7 @@ int run_bfs(tsw_ctx* c, const uint32_t* goals, const uint32_t* slots, uint32_t k
     A.H = c->G.H;
     A.Bp = c->Bp;
     A.nbp = c->nbp;
+    A.bp_magic = (uint32_t)((0xFFFFFFFFull + c->Bp) / c->Bp);
     A.frb = c->d_frb;
     A.abase = c->d_abase;
     A.nrs = std::max<uint32_t>(c->nrs, 1u);

@@ -99,7 +99,7 @@ hipError_t launch_bfs_big(const BigBfsArgs& A, int max_lds, int num_cu, hipStrea
 // K1 v5 (tsw_bfs_mg.hip): one WORKGROUP per group of <= 16 same-parity goals, a u16 goal mask per
 // cell in LDS; blocks numbered as k_bfs_blk (frb, abase shared with it).
 struct MgBfsArgs {
-  uint32_t W, H, Bp, nbp;
+  uint32_t W, H, Bp, nbp, bp_magic;  // bp_magic = ceil(2^32 / Bp): exact p / Bp for the block indices
   const uint64_t* frb;    // [nbp] padded free-cell blocks
   const uint32_t* abase;  // [nbp] first run-start index of block p
   uint32_t nrs;           // run starts in the grid
