@@ -29,10 +29,10 @@ Extra objects on the line:
                 prefix of the same instance on one pinned host core, rank 0 only; its prefix is
                 also compared bit-exactly with the GPU plan, and the GPU plans the SAME prefix
                 (same max_t, from an empty table store) for a like-for-like rate.
-  sharded_plan  N > 1 only: the north_star multi-GPU pipeline on rank 0's instance — every rank
-                builds its goal shard of the plan's K1 tables, RCCL all-gather over xGMI, rank 0
-                imports them into its planning context and plans (max over ranks of the whole
-                pipeline), bit-exact against rank 0's replica plan.
+  sharded_plan  N > 1 only: C5 (configs[4]) planned once on rank 0 with its K3 sharded per step by
+                goal owner across all ranks (tsw_plan_mapd_resolved + sharding.ShardedK3, RCCL),
+                timed against rank 0's replica plan of C5 alone, bit-exact against it. The goal-
+                sharded K1 + all-gather is in the `bfs` object (den520d).
 """
 from __future__ import annotations
 
@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-bfs", action="store_true", help="skip the K1 BFS measurement")
     ap.add_argument("--no-plan", action="store_true", help="skip the planning leg (profiling K1 alone)")
+    ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the sharded-K3 C5 leg")
     ap.add_argument("--bfs-goals", type=int, default=10000)
     ap.add_argument("--bfs-reps", type=int, default=3)
     ap.add_argument("--cpu-steps", type=int, default=300,
@@ -196,61 +197,64 @@ def goal_set(rows, starts, tasks) -> np.ndarray:
     return np.unique(c.astype(np.uint32))
 
 
-def sharded_plan_leg(args, rows, n_agents, n_tasks, seed, rank, world, dev, dist, barrier, allmax, ref_rec):
-    """north_star multi-GPU pipeline: rank 0's instance planned with its goal tables
-    built goal-sharded on all ranks (K1 into a torch tensor, tsw_dist_tables_device), RCCL
-    all-gather over xGMI (sharding.build_and_allgather), tsw_import_tables_device into rank 0's
-    PLANNING context, then tsw_plan_mapd there — all inside the timed region, max over ranks. The
-    step itself does not shard: the other ranks only build and send tables."""
-    import torch
-
+def sharded_plan_leg(args, rank, world, dev, dist, barrier, allmax):
+    """N > 1: the multi-GPU pipeline on the instance where the planner's time is K3 — C5 (BASELINE
+    configs[4]: 1024x1024 sortation floor, 10,000 agents, dense rotations; ~1M exact-A* queries per
+    plan) — planned ONCE on rank 0 with its K3 sharded per step by goal owner:
+    tsw_plan_mapd_resolved runs the planner in exit mode and hands every stop's batch of (start, goal)
+    pairs to sharding.ShardedK3, which broadcasts it, lets the rank owning each goal (goal % N) answer
+    from its own table store (tsw_next_hop_codes: K1 + exact A* for its goals only) and gathers the
+    u8 codes with one all-reduce(MIN) over RCCL. Timed against the replica plan of the same instance
+    on rank 0 alone (coop mode: K3 workers inside the plan dispatch), bit-exact against it. K1 tables
+    are NOT all-gathered here: C5's 17,885 tables are 36 GB of u16, more than the 279 ms they take to
+    build (the `bfs` object carries the goal-sharded K1 + all-gather on den520d)."""
     from p2p_distributed_tswap_amd import Planner, maps, sharding
 
-    starts, tasks = maps.make_instance(rows, n_agents, n_tasks, seed)  # rank 0's replica instance
-    goals = goal_set(rows, starts, tasks)
-    ncell = len(rows) * len(rows[0])
-    p = Planner(rows, device=dev)
-    build = lambda g, o: p.dist_tables_device(g, o.data_ptr())  # noqa: E731
-    times, parts, rec = [], [], None
-    for rep in range(max(args.steps, 1) + 1):  # first repetition = warm-up
-        p.clear_tables()
-        p.reset_stats()
+    rows, starts, tasks = maps.c5_instance()
+    n = starts.shape[0]
+    owner = Planner(rows, device=dev)
+    planner = Planner(rows, device=dev) if rank == 0 else None
+    ref_rec, replica_s = None, None
+    if rank == 0:
+        planner.plan_mapd_arrays(starts[:8], tasks[:8], 4)  # context warm-up
+        planner.clear_tables()
+        t0 = time.perf_counter()
+        ref_rec, _ = planner.plan_mapd_arrays(starts, tasks, 2000)
+        replica_s = time.perf_counter() - t0
+    times, rec, stops, pairs = [], None, 0, 0
+    for rep in range(2):  # warm-up + one timed plan (a C5 plan is seconds)
+        owner.clear_tables()
+        if planner is not None:
+            planner.clear_tables()
+            planner.reset_stats()
         barrier()
         t0 = time.perf_counter()
-        full = sharding.build_and_allgather(goals, ncell, rank, world, build, dist, "cuda")
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        if rank == 0:
-            p.reset_stats()  # from here on: the planning context's own work (imports + plan)
-            for _, gl, off in sharding.gathered_blocks(goals, world):
-                if gl.size:
-                    p.import_tables_device(gl, full[off:off + gl.size].data_ptr())
-            t2 = time.perf_counter()
-            rec, _ = p.plan_mapd_arrays(starts, tasks, 2000)
-            t3 = time.perf_counter()
-        else:
-            t2 = t3 = t1
-        del full
+        res, sk = sharding.plan_sharded_k3(
+            rank, world, dist, "cuda" if args.dist_backend == "nccl" else "cpu", owner.next_hop_codes,
+            (lambda r: planner.plan_mapd_resolved(starts, tasks, 2000, r)) if rank == 0 else None)
         barrier()
         dt = allmax(time.perf_counter() - t0)
-        if rep > 0:
+        if rep == 1:
             times.append(dt)
-            parts.append((t1 - t0, t2 - t1, t3 - t2))
-    st = p.stats()  # rank 0: the last repetition's import + plan
-    p.close()
+            stops, pairs = sk.stops, sk.pairs
+            if rank == 0:
+                rec = res[0]
+    st = planner.stats() if planner is not None else None
+    owner.close()
+    if planner is not None:
+        planner.close()
     if rank != 0:
         return None
-    n = len(times)
     return {
-        "instance": f"{args.config} seed {seed} (rank 0's replica)",
-        "goals": int(goals.size), "goals_per_rank": int(sharding.shard_rows(goals.size, world)),
-        "sharded_plan_ms": round(1e3 * sum(times) / n, 3),
-        "k1_shard_build_allgather_ms": round(1e3 * sum(x[0] for x in parts) / n, 3),
-        "import_ms": round(1e3 * sum(x[1] for x in parts) / n, 3),
-        "plan_ms": round(1e3 * sum(x[2] for x in parts) / n, 3),
-        "agent_steps_per_s": round(n_agents * rec.shape[1] / (sum(times) / n), 1),
-        "planning_context_k1_goals": int(st["bfs_goals"]),  # 0: every table came from the all-gather
-        "bit_exact_vs_replica_plan": bool(ref_rec is not None and rank == 0 and np.array_equal(rec, ref_rec)),
+        "instance": "c5_sortation_1024_10k (BASELINE configs[4]): 1024x1024, 10,000 agents, 10,000 tasks, cap 2000",
+        "k3": f"per-step batches sharded by goal owner (goal % {world}) over {args.dist_backend}, all-reduce(MIN) of u8 codes",
+        "sharded_plan_s": round(times[0], 3),
+        "replica_plan_s_rank0_alone": round(replica_s, 3),
+        "speedup_vs_replica": round(replica_s / times[0], 3),
+        "agent_steps_per_s": round(n * rec.shape[1] / times[0], 1),
+        "planner_stops": int(stops), "k3_pairs_resolved_by_owners": int(pairs),
+        "planner_k1_goals": int(st["bfs_goals"]), "planner_section_ms": [round(x, 1) for x in st["plan_section_ms"]],
+        "bit_exact_vs_replica_plan": bool(ref_rec is not None and np.array_equal(rec, ref_rec)),
         "backend": args.dist_backend,
     }
 
@@ -395,9 +399,8 @@ def main():
         latency = latency_roofline(st, us_wave, us_pass)
 
     sharded = None
-    if world > 1 and not args.no_plan:
-        sharded = sharded_plan_leg(args, rows, n_agents, n_tasks, seed, rank, world, dev, dist, barrier, allmax,
-                                   last_rec)
+    if world > 1 and not args.no_plan and not args.no_sharded:
+        sharded = sharded_plan_leg(args, rank, world, dev, dist, barrier, allmax)
 
     # K1 BFS alone, den520d-like, 10k distinct goals (configs[3]); rank-local shard of the goals
     bfs = None
