@@ -81,6 +81,7 @@ struct Tunables {
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
   bool dag_exit = true;           // TSW_DAG_EXIT=0: coop workers' A* runs to the goal's pop (no DAG early exit)
   uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
+  uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
   uint64_t worker_idle_us = 5000000;  // TSW_WORKER_IDLE_US: an idle coop worker exits after this long (test knob)
 
   static Tunables from_env() {
@@ -123,6 +124,7 @@ struct Tunables {
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
     t.dag_exit = num("TSW_DAG_EXIT", 0, 1, 1) != 0;
     t.dag_mask = (uint32_t)num("TSW_DAG_MASK", 0, 0x7FFFFFFF, t.dag_mask);
+    t.stale_steps = (uint32_t)num("TSW_SPEC_STALE", 0, 1 << 20, t.stale_steps);
     t.worker_idle_us = (uint64_t)num("TSW_WORKER_IDLE_US", 1, 5000000, (long)t.worker_idle_us);
 #endif
     return t;
@@ -1232,6 +1234,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.tasks_lds = tk;
   // coop mode: lazy next hops only (eager tables have nothing left to resolve)
   P.coop = (c->tun.coop && !c->resolver && P.prefetch && c->d_cc && c->d_QS) ? 1u : 0u;
+  P.stale_steps = c->tun.stale_steps;
   P.hflags = c->d_flags;  // watchdog words, both modes
   if (P.coop) {
     P.QS = c->d_QS;
@@ -1453,6 +1456,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                   "MOVE %u/%u | PRE1 never queued: assigned %u, picked up %u | chain queries %llu of %llu\n", cc.dbg_need[0], cc.dbg_need[1], cc.dbg_need[2],
                   cc.dbg_need[3], cc.dbg_need[4], cc.dbg_need[5], cc.dbg_need[6], cc.dbg_need[7],
                   (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
+          fprintf(stderr, "[k_plan] speculative pairs dropped as stale: %u (threshold %u ticks)\n", cc.spec_dropped,
+                  cc.stale_ticks);
           fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u | queue delay enqueue -> claim: needed "
                   "avg %.1f us (%u > 1 ms, %u already resolved), speculative avg %.1f us (%u > 1 ms, %u already resolved)\n",
                   cc.waits ? (double)cc.dbg_depth / cc.waits : 0.0, cc.dbg_depth_max,

@@ -91,7 +91,13 @@ struct CoopCtl {
   uint32_t qskip[2];             // claimed pairs already resolved when claimed (not searched again)
   // diagnostics: speculative-queue backlog (published - claimed) when a planner wait starts
   unsigned long long dbg_depth;
-  uint32_t dbg_depth_max, pad4[3];
+  uint32_t dbg_depth_max;
+  // speculative entries older than this (wall ticks, 100 MHz; 0 = never) are dropped unresolved at
+  // claim time (their code goes back PENDING_S -> UNKNOWN): the planner publishes stale_steps x its
+  // running step time after every timestep
+  uint32_t stale_ticks;
+  uint32_t spec_dropped;  // ... entries dropped that way
+  uint32_t pad4;
 };
 
 struct AstarQuery {

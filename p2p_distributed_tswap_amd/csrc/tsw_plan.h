@@ -46,6 +46,7 @@ struct PlanArgs {
   uint32_t n, m, W, ncell;
   uint32_t mode, agents_lds, occ_lds, tasks_lds;
   uint32_t has_dups, prefetch;  // prefetch: enqueue rules-round next hops up front (rules_prefetch)
+  uint32_t stale_steps;         // coop: speculative entries older than this many timesteps are dropped (0: never)
   uint32_t f_lds;               // F1/F2 carved in LDS although the agent arrays are global
   uint32_t mu_lds;              // occ_lds and the movement rounds' MU words in LDS too
   uint32_t part_lds;            // !agents_lds: PART_* agent arrays carved in LDS anyway (flat accesses)

@@ -757,6 +757,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
   __shared__ unsigned long long s_tick[32], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
   __shared__ uint32_t s_bad;               // ASSIGN looked up an off-grid/blocked task cell
+  __shared__ unsigned long long s_tstep, s_tema;  // coop: wall clock of the last step end, step time EMA
   __shared__ uint32_t s_nassign, s_npick;  // diagnostics: this step's assignments / pickup arrivals
   const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6, nwaves = bd >> 6;
   const uint32_t n = P.n, W = P.W;
@@ -870,6 +871,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     s_ctl.status = PLAN_RUNNING;
     s_exit = 0;
     s_abort = 0;
+    s_tstep = 0ull;
+    s_tema = 0ull;
     s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     s_q[1] = 0;  // speculative queue (coop mode)
     s_q[2] = 0;  // publishes (coop mode)
@@ -2013,6 +2016,20 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       if (tid == 0) {
         s_ctl.t = t + 1;
         s_ctl.steps_run += 1;
+        if (P.coop && P.stale_steps) {
+          // speculation older than stale_steps timesteps (at the running step time) is dropped by the
+          // workers: a FIFO backlog of stale prefetches otherwise holds them while needed pairs wait
+          // (C5: 100k-entry backlog, 420 ms average age at claim, 4 ms per timestep)
+          const unsigned long long now = wall_clock64();
+          if (s_tstep != 0ull) {
+            const unsigned long long dt = now - s_tstep;
+            s_tema = s_tema == 0ull ? dt : (s_tema * 7ull + dt) >> 3;
+            const unsigned long long st = s_tema * P.stale_steps;
+            __hip_atomic_store(&P.cc->stale_ticks, (uint32_t)(st < 0xFFFFFFFFull ? st : 0xFFFFFFFFull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          s_tstep = now;
+        }
         if (P.hflags) __hip_atomic_store(&P.hflags[2], s_ctl.steps_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((s_ctl.unused == 0u && !busy) || s_ctl.t > s_ctl.max_t) {
           s_ctl.status = PLAN_DONE;

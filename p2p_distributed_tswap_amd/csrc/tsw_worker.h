@@ -289,6 +289,29 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     const uint32_t w = w_ld(reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u));
     return (uint8_t)(w >> (8u * (uint32_t)((uintptr_t)p & 3u)));
   };
+  // a speculative entry older than the planner's stale threshold is dropped unresolved: its code goes
+  // back PENDING_S -> UNKNOWN (CAS on the word, agent scope, so a code published meanwhile or a
+  // promotion to PENDING by the planner is never overwritten), and the planner queues the pair again
+  // if a step still needs it — results-neutral, only the workers' time is saved
+  auto drop_stale = [&](const uint32_t* e, uint32_t v, int32_t tab) -> bool {
+    if (tab < 0) return false;
+    bool drop = false;
+    if (lane == 0) {
+      const uint32_t st = w_ld(&A.cc->stale_ticks);
+      if (st != 0u && (uint32_t)wall_clock64() - w_ld(e + 3) > st) {
+        uint32_t* wp = reinterpret_cast<uint32_t*>((uintptr_t)(A.nh + (uint64_t)tab * A.nstride + v) & ~(uintptr_t)3u);
+        const uint32_t sh = 8u * (uint32_t)((uintptr_t)(A.nh + (uint64_t)tab * A.nstride + v) & 3u);
+        for (;;) {
+          const uint32_t w = w_ld(wp);
+          if (((w >> sh) & 0xFFu) != NH_PENDING_S) break;  // resolved, promoted or reset already
+          if (w_cas(wp, w, w | (0xFFu << sh))) break;     // NH_UNKNOWN = 0xFF
+        }
+        __hip_atomic_fetch_add(&A.cc->spec_dropped, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        drop = true;
+      }
+    }
+    return __builtin_amdgcn_readfirstlane(drop ? 1 : 0) != 0;
+  };
   const bool take_t = (wid & A.tmask) == A.tmask;
   for (;;) {
     int which = -1;
@@ -310,6 +333,7 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
         if (lane == 0) __hip_atomic_fetch_add(&A.cc->qskip[which], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         continue;
       }
+      if (which == 1 && drop_stale(e, v, tab)) continue;
       if (lane == 0) {  // diagnostics: queue delay (enqueue time in the entry's out word)
         const uint32_t dt = (uint32_t)wall_clock64() - w_ld(e + 3);
         __hip_atomic_fetch_add(&A.cc->qdelay[which], (unsigned long long)dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -338,6 +362,7 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
         const uint32_t* e2 = reinterpret_cast<const uint32_t*>((w2 == 0 ? A.QN : A.QS) + i2);
         const uint32_t v2 = w_ld(e2), g2 = w_ld(e2 + 1);
         const int32_t t2 = (int32_t)w_ld(e2 + 2);
+        if (w2 == 1 && drop_stale(e2, v2, t2)) continue;
         cur_q = (uint32_t)w2;
         publish_code(v2, t2, resolve(v2, g2, t2), false);
         cur_q = 2u;

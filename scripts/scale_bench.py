@@ -122,7 +122,9 @@ def main():
             "coop_waits": st["coop_waits"], "coop_wait_ms": round(st["coop_wait_ms"], 2),
             "coop_wait_sec_ms": [round(x, 2) for x in st["coop_wait_sec_ms"]],
             "coop_waits_sec": st["coop_waits_sec"], "relabels_full": st["relabels_full"],
-            "relabels_inc": st["relabels_inc"], "env": {k: v for k, v in os.environ.items() if k.startswith("TSW_")},
+            "relabels_inc": st["relabels_inc"], "coop_workers": st["coop_workers"],
+            "coop_worker_busy_ms": [round(x, 1) for x in st["coop_worker_busy_ms"]],
+            "env": {k: v for k, v in os.environ.items() if k.startswith("TSW_")},
         }
         print(json.dumps(out), flush=True)
 
