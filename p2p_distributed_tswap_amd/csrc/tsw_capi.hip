@@ -1234,7 +1234,6 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.tasks_lds = tk;
   // coop mode: lazy next hops only (eager tables have nothing left to resolve)
   P.coop = (c->tun.coop && !c->resolver && P.prefetch && c->d_cc && c->d_QS) ? 1u : 0u;
-  P.stale_steps = c->tun.stale_steps;
   P.hflags = c->d_flags;  // watchdog words, both modes
   if (P.coop) {
     P.QS = c->d_QS;
@@ -1320,6 +1319,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     // the test's heap scan gathers D from LDS (detour bytes) or from the u16 table in global memory:
     // every 16 / 64 pops (C3 worker busy -20 %, wh10k 400 steps 5.77 -> 5.42 s; profiles/r3/dag_exit_ab.txt)
     W.dag_mask = c->tun.dag_mask ? c->tun.dag_mask : (W.dag == 1u ? 15u : 63u);
+    W.stale_steps = c->tun.stale_steps;
     W.idle_ticks = c->tun.worker_idle_us * 100ull;  // wall clock: 100 MHz
     W.dist = c->d_dist;
     W.gs_lds = wcfg.gs_lds;
@@ -1456,13 +1456,13 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                   "MOVE %u/%u | PRE1 never queued: assigned %u, picked up %u | chain queries %llu of %llu\n", cc.dbg_need[0], cc.dbg_need[1], cc.dbg_need[2],
                   cc.dbg_need[3], cc.dbg_need[4], cc.dbg_need[5], cc.dbg_need[6], cc.dbg_need[7],
                   (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
-          fprintf(stderr, "[k_plan] speculative pairs dropped as stale: %u (threshold %u ticks)\n", cc.spec_dropped,
-                  cc.stale_ticks);
+          fprintf(stderr, "[k_plan] speculative pairs dropped as stale: %u (older than %u timesteps)\n",
+                  cc.spec_dropped, c->tun.stale_steps);
           fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u | queue delay enqueue -> claim: needed "
-                  "avg %.1f us (%u > 1 ms, %u already resolved), speculative avg %.1f us (%u > 1 ms, %u already resolved)\n",
+                  "avg %.1f us (%u > 1 ms, %u already resolved), speculative avg %.1f timesteps (%u > 1, %u already resolved)\n",
                   cc.waits ? (double)cc.dbg_depth / cc.waits : 0.0, cc.dbg_depth_max,
                   cc.wcount[0] ? cc.qdelay[0] / 100.0 / cc.wcount[0] : 0.0, cc.qlate[0], cc.qskip[0],
-                  cc.wcount[1] ? cc.qdelay[1] / 100.0 / cc.wcount[1] : 0.0, cc.qlate[1], cc.qskip[1]);
+                  cc.wcount[1] ? (double)cc.qdelay[1] / cc.wcount[1] : 0.0, cc.qlate[1], cc.qskip[1]);
           fprintf(stderr, "[k_plan] worker A* ms (queries, pops): needed %.1f (%u, %llu) spec %.1f (%u, %llu) task chains "
                   "%.1f (%u, %llu) | tier-2 hand-offs %llu tier-3 %llu | detour staging %.1f ms (%u)\n",
                   cc.wbusy[0] / (double)c->wall_khz, cc.wcount[0], cc.wpops[0], cc.wbusy[1] / (double)c->wall_khz,

@@ -92,10 +92,10 @@ struct CoopCtl {
   // diagnostics: speculative-queue backlog (published - claimed) when a planner wait starts
   unsigned long long dbg_depth;
   uint32_t dbg_depth_max;
-  // speculative entries older than this (wall ticks, 100 MHz; 0 = never) are dropped unresolved at
-  // claim time (their code goes back PENDING_S -> UNKNOWN): the planner publishes stale_steps x its
-  // running step time after every timestep
-  uint32_t stale_ticks;
+  // the planner's current timestep (agent-scope store at every step end): speculative entries carry
+  // their enqueue timestep, and a worker drops one older than WorkerArgs::stale_steps unresolved
+  // (its code goes back PENDING_S -> UNKNOWN)
+  uint32_t t_now;
   uint32_t spec_dropped;  // ... entries dropped that way
   uint32_t pad4;
 };

@@ -46,7 +46,6 @@ struct PlanArgs {
   uint32_t n, m, W, ncell;
   uint32_t mode, agents_lds, occ_lds, tasks_lds;
   uint32_t has_dups, prefetch;  // prefetch: enqueue rules-round next hops up front (rules_prefetch)
-  uint32_t stale_steps;         // coop: speculative entries older than this many timesteps are dropped (0: never)
   uint32_t f_lds;               // F1/F2 carved in LDS although the agent arrays are global
   uint32_t mu_lds;              // occ_lds and the movement rounds' MU words in LDS too
   uint32_t part_lds;            // !agents_lds: PART_* agent arrays carved in LDS anyway (flat accesses)
@@ -140,6 +139,7 @@ struct WorkerArgs {
   uint32_t dag;
   const uint16_t* dist;  // K1 tables, nstride entries per goal slot
   uint32_t dag_mask;     // the DAG test runs when (pops & dag_mask) == 0
+  uint32_t stale_steps;  // speculative entries queued more than this many timesteps ago are dropped (0: never)
   unsigned long long idle_ticks;  // a worker idle this long (100 MHz ticks) exits (5 s)
 };
 // Worker placement: per-wave LDS (heap, g-scores, free bitmap) sets the waves per CU. g-scores stay

@@ -309,7 +309,7 @@ __device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uin
     q.v = v;
     q.goal = g;
     q.tab = tab;
-    q.out = (uint32_t)wall_clock64();  // enqueue time (diagnostics)
+    q.out = s_q[5];  // enqueue timestep: the workers drop entries older than stale_steps
     P.QS[qi] = q;
     return;
   }
@@ -750,14 +750,13 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     return;
   }
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[5], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
+  __shared__ uint32_t s_q[6], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
   __shared__ uint32_t s_ap[128];  // rules: members of a rule-4 cycle rotated by the wave (<= 64), links
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ unsigned long long s_tick[32], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
   __shared__ uint32_t s_bad;               // ASSIGN looked up an off-grid/blocked task cell
-  __shared__ unsigned long long s_tstep, s_tema;  // coop: wall clock of the last step end, step time EMA
   __shared__ uint32_t s_nassign, s_npick;  // diagnostics: this step's assignments / pickup arrivals
   const uint32_t tid = threadIdx.x, bd = blockDim.x, lane = tid & 63u, wid = tid >> 6, nwaves = bd >> 6;
   const uint32_t n = P.n, W = P.W;
@@ -871,13 +870,13 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     s_ctl.status = PLAN_RUNNING;
     s_exit = 0;
     s_abort = 0;
-    s_tstep = 0ull;
-    s_tema = 0ull;
     s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     s_q[1] = 0;  // speculative queue (coop mode)
     s_q[2] = 0;  // publishes (coop mode)
     s_q[3] = 0;  // last published needed / speculative heads (coop mode)
     s_q[4] = 0;
+    s_q[5] = s_ctl.t;  // the timestep speculative entries are queued in (coop mode)
+    if (P.coop) __hip_atomic_store(&P.cc->t_now, s_ctl.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int k = 0; k < 32; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
@@ -2016,20 +2015,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       if (tid == 0) {
         s_ctl.t = t + 1;
         s_ctl.steps_run += 1;
-        if (P.coop && P.stale_steps) {
-          // speculation older than stale_steps timesteps (at the running step time) is dropped by the
-          // workers: a FIFO backlog of stale prefetches otherwise holds them while needed pairs wait
-          // (C5: 100k-entry backlog, 420 ms average age at claim, 4 ms per timestep)
-          const unsigned long long now = wall_clock64();
-          if (s_tstep != 0ull) {
-            const unsigned long long dt = now - s_tstep;
-            s_tema = s_tema == 0ull ? dt : (s_tema * 7ull + dt) >> 3;
-            const unsigned long long st = s_tema * P.stale_steps;
-            __hip_atomic_store(&P.cc->stale_ticks, (uint32_t)(st < 0xFFFFFFFFull ? st : 0xFFFFFFFFull),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          s_tstep = now;
-        }
+        // speculative entries carry their enqueue timestep (s_q[5]); the workers drop the stale ones
+        s_q[5] = t + 1;
+        if (P.coop) __hip_atomic_store(&P.cc->t_now, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (P.hflags) __hip_atomic_store(&P.hflags[2], s_ctl.steps_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((s_ctl.unused == 0u && !busy) || s_ctl.t > s_ctl.max_t) {
           s_ctl.status = PLAN_DONE;

@@ -296,9 +296,8 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   auto drop_stale = [&](const uint32_t* e, uint32_t v, int32_t tab) -> bool {
     if (tab < 0) return false;
     bool drop = false;
-    if (lane == 0) {
-      const uint32_t st = w_ld(&A.cc->stale_ticks);
-      if (st != 0u && (uint32_t)wall_clock64() - w_ld(e + 3) > st) {
+    if (lane == 0 && A.stale_steps != 0u) {
+      if (w_ld(&A.cc->t_now) - w_ld(e + 3) > A.stale_steps) {
         uint32_t* wp = reinterpret_cast<uint32_t*>((uintptr_t)(A.nh + (uint64_t)tab * A.nstride + v) & ~(uintptr_t)3u);
         const uint32_t sh = 8u * (uint32_t)((uintptr_t)(A.nh + (uint64_t)tab * A.nstride + v) & 3u);
         for (;;) {
@@ -334,10 +333,11 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
         continue;
       }
       if (which == 1 && drop_stale(e, v, tab)) continue;
-      if (lane == 0) {  // diagnostics: queue delay (enqueue time in the entry's out word)
-        const uint32_t dt = (uint32_t)wall_clock64() - w_ld(e + 3);
+      if (lane == 0) {  // diagnostics: queue delay (needed: enqueue wall time, speculative: timestep)
+        const uint32_t dt = (which == 0 ? (uint32_t)wall_clock64() : w_ld(&A.cc->t_now)) - w_ld(e + 3);
         __hip_atomic_fetch_add(&A.cc->qdelay[which], (unsigned long long)dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (dt > 100000u) __hip_atomic_fetch_add(&A.cc->qlate[which], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dt > (which == 0 ? 100000u : 1u))
+          __hip_atomic_fetch_add(&A.cc->qlate[which], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       publish_code(v, tab, resolve(v, goal, tab), false);
       continue;
