@@ -48,7 +48,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md ("HBM: 8 TB/s peak")
-PROFILE_TAG = "r3"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
+PROFILE_TAG = "r4"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
 BFS_WORKLOAD = "bfs:den520d_10k"
 
 
@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--no-bfs", action="store_true", help="skip the K1 BFS measurement")
     ap.add_argument("--no-plan", action="store_true", help="skip the planning leg (profiling K1 alone)")
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the sharded-K3 C5 leg")
+    ap.add_argument("--exit-mode", action="store_true",
+                    help="TSW_F_EXIT_MODE: no K3 workers in the plan dispatch (K3 as host-launched passes) — "
+                         "the profile's planner-only traffic (VERDICT r3 #7), not the headline")
     ap.add_argument("--bfs-goals", type=int, default=10000)
     ap.add_argument("--bfs-reps", type=int, default=3)
     ap.add_argument("--cpu-steps", type=int, default=300,
@@ -89,6 +92,34 @@ def profiled_traffic(workload: str, kclass: str, algo_bytes_per_launch: float):
     if a <= 0 or abs(a - algo_bytes_per_launch) > 0.02 * algo_bytes_per_launch or "hbm_bytes_per_launch" not in d:
         return None, None
     return float(d["hbm_bytes_per_launch"]), os.path.relpath(p, ROOT)
+
+
+def traffic_split(config: str, coop_traffic, steps: int, queries: int):
+    """the coop plan dispatch carries the planner AND its K3 workers, so its PMC bytes
+    are split with the same plan profiled in exit mode (profiles/<tag>/pmc.json workload plan_exit:
+    the planner's k_plan dispatches alone, K3 as separate host-launched passes): planner bytes per
+    agent-step from there, worker bytes = the coop dispatch's bytes minus the planner's, per query."""
+    p = os.path.join(ROOT, "profiles", PROFILE_TAG, "pmc.json")
+    try:
+        with open(p) as f:
+            wl = json.load(f)["workloads"][f"plan_exit:{config}"]
+        kp, k3 = wl["k_plan"], wl.get("K3", {})
+        planner_total = kp["hbm_bytes_per_launch"] * kp["launches"]
+        exit_steps = kp["agent_steps"]
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+    out = {"source": os.path.relpath(p, ROOT),
+           "planner_bytes_per_agent_step": round(planner_total / max(exit_steps, 1), 2),
+           "planner_algorithmic_bytes_per_agent_step": 46.0,
+           "exit_mode_k3_bytes_per_query": (round(k3["hbm_bytes_per_launch"] * k3["launches"] / max(k3["queries"], 1), 1)
+                                            if "hbm_bytes_per_launch" in k3 and k3.get("queries") else None)}
+    if coop_traffic is not None and steps and queries:
+        planner_part = out["planner_bytes_per_agent_step"] * steps  # steps: agent-steps of one launch
+        out["coop_dispatch_bytes"] = round(coop_traffic, 1)
+        out["planner_part_bytes"] = round(planner_part, 1)
+        out["workers_part_bytes"] = round(coop_traffic - planner_part, 1)
+        out["workers_bytes_per_query"] = round((coop_traffic - planner_part) / queries, 1)
+    return out
 
 
 def bfs_bytes_per_goal(w: int, h: int, with_nh: bool) -> int:
@@ -276,7 +307,7 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    from p2p_distributed_tswap_amd import TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP, Planner, maps
+    from p2p_distributed_tswap_amd import TSW_F_EAGER_NEXTHOP, TSW_F_EXIT_MODE, TSW_F_LAZY_NEXTHOP, Planner, maps
 
     def barrier():
         if dist is not None:
@@ -301,12 +332,14 @@ def main():
     rows = fac()
     h, w = len(rows), len(rows[0])
     starts, tasks = maps.make_instance(rows, n_agents, n_tasks, seed + rank)
-    workload = f"plan:{args.config}"
+    workload = f"{'plan_exit' if args.exit_mode else 'plan'}:{args.config}"
 
     value = dt_max = None
     Ts, st, roofline, latency, last_rec = [], {}, None, None, None
     if not args.no_plan:
         pflags = {"auto": 0, "eager": TSW_F_EAGER_NEXTHOP, "lazy": TSW_F_LAZY_NEXTHOP}[args.nexthop]
+        if args.exit_mode:
+            pflags |= TSW_F_EXIT_MODE
         planner = Planner(rows, device=dev, flags=pflags)
 
         def one_plan():
@@ -396,6 +429,10 @@ def main():
                      "construction and their binding limit is latency (see `latency`). K1 (bfs.roofline) is the "
                      "HBM-bound kernel." if dom != "K1" else None),
         }
+        plans = max(int(st["walker_launches"]), 1) if dom == "k_plan" else max(args.steps, 1)
+        roofline["traffic_split"] = (traffic_split(args.config, traffic, n_agents * steps_total / plans,
+                                                   st["astar_queries"] / plans)
+                                     if dom == "k_plan" and not args.exit_mode else None)
         latency = latency_roofline(st, us_wave, us_pass)
 
     sharded = None

@@ -38,7 +38,7 @@ for step in "$@"; do
     scale:*) n=${step#scale:}; run 1100 python -u scripts/scale_bench.py $n > gpurun_out/scale_$n.jsonl 2> gpurun_out/scale_$n.log || exit $? ;;
     scaleT:*) a=${step#scaleT:}; n=${a%%:*}; t=${a#*:}
       run 900 python -u scripts/scale_bench.py $n --max-t $t > gpurun_out/scale_${n}_t$t.jsonl 2> gpurun_out/scale_${n}_t$t.log || exit $? ;;
-    profile) bash scripts/profile_round.sh r3 || exit $? ;;
+    profile) bash scripts/profile_round.sh r4 || exit $? ;;
     astar) run 300 python scripts/astar_bench.py --out gpurun_out/astar_bench.json > gpurun_out/astar_bench.log 2>&1 || exit $? ;;
     bfs) run 300 python scripts/bfs_bench.py 10000 5 cave > gpurun_out/bfs_bench.log 2>&1 &&
          run 300 python scripts/bfs_bench.py 2048 3 sort >> gpurun_out/bfs_bench.log 2>&1 || exit $? ;;

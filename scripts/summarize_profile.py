@@ -34,7 +34,8 @@ import os
 import shutil
 import sys
 
-WORKLOADS = {"plan": "plan:c3_warehouse_170x84", "bfs": "bfs:den520d_10k"}
+WORKLOADS = {"plan": "plan:c3_warehouse_170x84", "plan_exit": "plan_exit:c3_warehouse_170x84",
+             "bfs": "bfs:den520d_10k"}
 
 
 def short(name: str) -> str:
@@ -81,7 +82,7 @@ def main(src: str, dst: str):
             cls[c]["dispatches"] += int(r["Calls"])
             cls[c]["kernels"][short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
         # launches and algorithmic bytes per launch as the bench counts them
-        if wl == "plan":
+        if wl in ("plan", "plan_exit"):
             ref = (line.get("roofline") or {}).get("classes", {})
             launches = {c: d["launches"] for c, d in ref.items()}
             algo = {c: d["algorithmic_bytes_per_launch"] for c, d in ref.items()}
@@ -126,6 +127,12 @@ def main(src: str, dst: str):
                 e["hbm_bytes_per_launch"] = e["read_bytes_per_launch"] + e["write_bytes_per_launch"]
                 if algo.get(c):
                     e["traffic_over_algorithmic"] = e["hbm_bytes_per_launch"] / algo[c]
+            if wl in ("plan", "plan_exit"):  # for the planner / worker traffic split (bench.traffic_split)
+                ks = line.get("kernel_stats", {})
+                if c == "k_plan":
+                    e["agent_steps"] = int(line["config"]["agents"]) * int(ks.get("steps", 0))
+                if c == "K3":
+                    e["queries"] = int(ks.get("astar_queries", 0))
             res[c] = e
         out["workloads"][key] = res
     bj = os.path.join(src, "bench.json")
