@@ -1408,9 +1408,12 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       c->st.coop_workers = W.nworkers;
       for (int k = 0; k < 3; ++k) c->st.coop_worker_busy_ms[k] += (double)cc.wbusy[k] / (double)c->wall_khz;
       if (cc.err) RET(TSW_EOVERFLOW, "K3 worker: A* heap overflow");
-      // speculative pairs nobody claimed stay PENDING_S: back to UNKNOWN for later calls
+      // speculative pairs nobody claimed stay PENDING_S: back to UNKNOWN for later calls — only the
+      // unclaimed queue entries (every claimed one was resolved, or reset by the worker that dropped
+      // it as stale): a whole-store sweep cost C5 ~4 s per call (18 GB of codes)
       if (cc.head_s > cc.claim_s) {
-        HIPCHK(launch_reset_pending(c->d_nh, (uint64_t)c->tab_count * c->tstride, c->s));
+        HIPCHK(launch_reset_queue(c->d_QS, cc.claim_s, std::min<uint32_t>(cc.head_s, (uint32_t)c->qscap), c->d_nh,
+                                  c->tstride, c->s));
         HIPCHK(hipStreamSynchronize(c->s));
       }
     }
@@ -2265,9 +2268,10 @@ int tsw_import_next_hops_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, c
       HIPCHK(hipMemcpyAsync(c->d_nh + (size_t)slots[j] * c->tstride, dev_nh + (size_t)src[j] * ncell, ncell,
                             hipMemcpyDeviceToDevice, c->s));
     }
-    // a pending marker from the producing context means "not resolved": unknown here (between
-    // calls no code of this store is pending, so one sweep over the whole store is exact)
-    HIPCHK(launch_reset_pending(c->d_nh, (uint64_t)c->tab_count * c->tstride, c->s));
+    // a pending marker from the producing context means "not resolved": unknown here — swept over
+    // the imported slots only (a whole-store sweep grows with every table the context holds)
+    for (size_t j = 0; j < newg.size(); ++j)
+      HIPCHK(launch_reset_pending(c->d_nh + (size_t)slots[j] * c->tstride, c->tstride, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     return TSW_OK;
   };

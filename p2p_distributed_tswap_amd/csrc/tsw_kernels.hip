@@ -728,6 +728,27 @@ hipError_t launch_put_codes(const AstarQuery* Q, uint32_t nq, const uint8_t* cod
   return hipGetLastError();
 }
 
+// The pending markers of queue entries [from, to) back to NH_UNKNOWN (a coop plan's unclaimed
+// speculative pairs): O(entries), where launch_reset_pending sweeps the whole store (C5: 18 GB).
+__global__ void k_reset_queue(const AstarQuery* __restrict__ Q, uint32_t from, uint32_t to, uint8_t* __restrict__ nh,
+                              uint64_t nstride) {
+  for (uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x; i < to; i += gridDim.x * blockDim.x) {
+    const AstarQuery q = Q[i];
+    if (q.tab < 0) continue;
+    uint8_t* p = nh + (uint64_t)q.tab * nstride + q.v;
+    const uint8_t c = *p;
+    if (c == NH_PENDING || c == NH_PENDING_S) *p = NH_UNKNOWN;
+  }
+}
+
+hipError_t launch_reset_queue(const AstarQuery* Q, uint32_t from, uint32_t to, uint8_t* nh, uint64_t nstride,
+                              hipStream_t s) {
+  if (to <= from) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>((to - from + 255u) / 256u, 4096u);
+  hipLaunchKernelGGL(k_reset_queue, dim3(grid), dim3(256), 0, s, Q, from, to, nh, nstride);
+  return hipGetLastError();
+}
+
 hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                                   uint8_t* nh, uint64_t nstride, AstarQuery* Q, uint32_t* qcount,
                                   uint32_t qcap, hipStream_t s) {

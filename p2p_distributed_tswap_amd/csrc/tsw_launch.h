@@ -154,6 +154,10 @@ hipError_t launch_gather_codes(const AstarQuery* Q, uint32_t nq, const uint8_t* 
 hipError_t launch_put_codes(const AstarQuery* Q, uint32_t nq, const uint8_t* codes, uint8_t* nh, uint64_t nstride,
                             hipStream_t s);
 
+// NH_PENDING(_S) -> NH_UNKNOWN for the pairs of queue entries [from, to)
+hipError_t launch_reset_queue(const AstarQuery* Q, uint32_t from, uint32_t to, uint8_t* nh, uint64_t nstride,
+                              hipStream_t s);
+
 // NH_PENDING -> NH_UNKNOWN over nbytes of next-hop codes (error recovery)
 hipError_t launch_reset_pending(uint8_t* nh, uint64_t nbytes, hipStream_t s);
 
