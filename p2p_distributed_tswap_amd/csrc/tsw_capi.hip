@@ -1579,8 +1579,16 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   }
   HIPCHK(hipMemcpyAsync(c->d_unused, &m, 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipStreamSynchronize(c->s));  // host vectors above go out of scope only at return, but keep it simple
+  auto tphase = [&](const char* what) {  // diagnostics (TSW_PLAN_DEBUG): host-side phases of the call
+    if (c->tun.plan_debug)
+      fprintf(stderr, "[plan] %s at %.1f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  };
+  tphase("inputs uploaded");
   TRY(build_occ(c, n));
   TRY(ensure_tables(c, goalset, true));
+  HIPCHK(hipStreamSynchronize(c->s));
+  tphase("tables built");
   TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
   c->qt_count = 0;
   if (c->tun.coop && !c->resolver && !eager_policy(c, 0)) {
@@ -1609,7 +1617,9 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   init.unused = m;
   init.max_t = max_t;
   init.chase_id = c->chase_id;
+  tphase("plan dispatch starts");
   TRY(run_plan(c, P, init));
+  tphase("plan dispatch done");
   const uint32_t t = c->h_ctl->t;
   c->st.steps += t;
   *out_T = t;
@@ -1915,7 +1925,9 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   PlanCtl init{};
   init.section = SEC_PRE1;
   init.chase_id = c->chase_id;
+  tphase("plan dispatch starts");
   TRY(run_plan(c, P, init));
+  tphase("plan dispatch done");
   HIPCHK(hipMemcpyAsync(v, c->d_v, n * 4ull, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipMemcpyAsync(g, c->d_g, n * 4ull, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipStreamSynchronize(c->s));
