@@ -1925,9 +1925,7 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   PlanCtl init{};
   init.section = SEC_PRE1;
   init.chase_id = c->chase_id;
-  tphase("plan dispatch starts");
   TRY(run_plan(c, P, init));
-  tphase("plan dispatch done");
   HIPCHK(hipMemcpyAsync(v, c->d_v, n * 4ull, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipMemcpyAsync(g, c->d_g, n * 4ull, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipStreamSynchronize(c->s));
