@@ -117,7 +117,10 @@ __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool tak
 
 // lane 0, non-blocking: claim one pair of the needed or the speculative queue (0 / 1), else -1.
 // A worker walking a task chain calls this between hops, so chains (lowest priority, up to ~100
-// A* each) never hold a worker while pairs the planner needs or will need soon are queued.
+// A* each) never hold a worker while pairs the planner needs or will need soon are queued. Once the
+// planner has stopped only needed pairs are taken (as in worker_claim): the chain workers' preempt
+// loop used to drain the whole speculative backlog after the plan ended (C5, 1 timestep: 4.2 s of
+// dispatch for 0.2 s of planning, 113k speculative A* nobody would read).
 __device__ __forceinline__ int worker_try_claim(CoopCtl* cc, uint32_t* idx) {
   for (;;) {
     const uint32_t hn = w_ld(&cc->head_n), cn = w_ld(&cc->claim_n);
@@ -128,6 +131,7 @@ __device__ __forceinline__ int worker_try_claim(CoopCtl* cc, uint32_t* idx) {
       }
       continue;
     }
+    if (w_ld(&cc->stop)) return -1;
     const uint32_t hs = w_ld(&cc->head_s), cs = w_ld(&cc->claim_s);
     if (cs < hs) {
       if (w_cas(&cc->claim_s, cs, cs + 1u)) {
