@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--no-bfs", action="store_true", help="skip the K1 BFS measurement")
     ap.add_argument("--no-plan", action="store_true", help="skip the planning leg (profiling K1 alone)")
     ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the sharded-K3 C5 leg")
+    ap.add_argument("--diag", action="store_true", help="diagnostic library (TSW_* A/B knobs; not the product)")
     ap.add_argument("--exit-mode", action="store_true",
                     help="TSW_F_EXIT_MODE: no K3 workers in the plan dispatch (K3 as host-launched passes) — "
                          "the profile's planner-only traffic (VERDICT r3 #7), not the headline")
@@ -340,7 +341,7 @@ def main():
         pflags = {"auto": 0, "eager": TSW_F_EAGER_NEXTHOP, "lazy": TSW_F_LAZY_NEXTHOP}[args.nexthop]
         if args.exit_mode:
             pflags |= TSW_F_EXIT_MODE
-        planner = Planner(rows, device=dev, flags=pflags)
+        planner = Planner(rows, device=dev, flags=pflags, diag=args.diag)
 
         def one_plan():
             planner.clear_tables()
