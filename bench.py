@@ -532,7 +532,8 @@ def main():
             "data": "synthetic (seeded warehouse-like map and MAPD task stream; replicas seed+rank)",
             "config": {
                 "workload": (f"{args.config}: {w}x{h} grid, {n_agents} agents, {n_tasks}-task MAPD stream, "
-                             "cap 2000, full plan from an empty table store per step (BASELINE configs[2])"),
+                             "cap 2000, full plan from an empty table store per step "
+                             f"(BASELINE configs[{list(maps.CONFIGS).index(args.config)}])"),
                 "agents": n_agents, "tasks": n_tasks, "grid": f"{w}x{h}",
                 "timesteps_per_plan": Ts, "parallelism": f"replicas x{world} (step not shardable)",
             },
