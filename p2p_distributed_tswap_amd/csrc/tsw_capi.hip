@@ -79,6 +79,7 @@ struct Tunables {
   bool avoid_xcc = true;          // TSW_WORKER_AVOID_XCD=0: coop workers also run on the planner's XCD
   bool chain_preempt = true;      // TSW_CHAIN_PREEMPT=0: chain workers finish a chain before serving queued pairs
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
+  int worker_fb = -1;             // TSW_WORKER_FB=0: global-g-score workers without the staged free bitmap (more waves per CU)
   bool dag_exit = true;           // TSW_DAG_EXIT=0: coop workers' A* runs to the goal's pop (no DAG early exit)
   uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
@@ -122,6 +123,7 @@ struct Tunables {
     t.chain_preempt = num("TSW_CHAIN_PREEMPT", 0, 1, 1) != 0;
     t.avoid_xcc = num("TSW_WORKER_AVOID_XCD", 0, 1, 1) != 0;
     t.worker_gs = (int)num("TSW_WORKER_GS", -1, 2, -1);
+    t.worker_fb = (int)num("TSW_WORKER_FB", -1, 1, -1);
     t.dag_exit = num("TSW_DAG_EXIT", 0, 1, 1) != 0;
     t.dag_mask = (uint32_t)num("TSW_DAG_MASK", 0, 0x7FFFFFFF, t.dag_mask);
     t.stale_steps = (uint32_t)num("TSW_SPEC_STALE", 0, 1 << 20, t.stale_steps);
@@ -1314,7 +1316,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.heaps = c->d_heaps;
     W.ghcap = c->hcap;
     const WorkerCfg wcfg =
-        worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs, c->tun.dag_exit, lds);
+        worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs, c->tun.dag_exit, lds, c->tun.worker_fb);
     W.dag = wcfg.dag;
     // the test's heap scan gathers D from LDS (detour bytes) or from the u16 table in global memory:
     // every 16 / 64 pops (C3 worker busy -20 %, wh10k 400 steps 5.77 -> 5.42 s; profiles/r3/dag_exit_ab.txt)

@@ -762,7 +762,7 @@ hipError_t launch_enqueue_unknown(const DevGrid& G, const uint32_t* goals, const
 
 
 WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs,
-                        bool dag_exit, size_t lds_cap) {
+                        bool dag_exit, size_t lds_cap, int force_fb) {
   // the workers' LDS is the plan dispatch's per-workgroup request (the planner's, just under the
   // CU's 160 KiB): every carve below must fit THAT, not the CU (C5's bitmap + heap
   // came to 160 KiB, 2 KiB over the dispatch's request, and no worker fit — exit mode)
@@ -813,6 +813,8 @@ WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_
   // larger grids keep one wave per CU with the bitmap in LDS: their 4 MB g-score slots would not
   // stay cache-resident with more waves, and the traffic slows the planner itself (C5: 3x)
   if (c.hcap < 64u) c = make(0u, false);
+  // A/B (TSW_WORKER_FB=0): global g-score grids without the staged bitmap, several waves per CU
+  if (force_fb == 0 && m == 0u) c = make(0u, false);
   return c;
 }
 

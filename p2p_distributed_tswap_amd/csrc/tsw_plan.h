@@ -151,7 +151,7 @@ struct WorkerCfg {
   size_t lds;
 };
 WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_t hcap_want, int force_gs = -1,
-                        bool dag_exit = true, size_t lds_cap = 160u * 1024u);
+                        bool dag_exit = true, size_t lds_cap = 160u * 1024u, int force_fb = -1);
 
 // The plan dispatch: workgroup 0 runs k_plan's planner (block threads, lds bytes of dynamic LDS);
 // with W (coop mode) workgroups 1..worker_blocks run W->wpb K3 worker waves each.
