@@ -372,6 +372,11 @@ __device__ __forceinline__ WinLane win_lane(uint32_t lane) {
 // lane-parallel (each lane tests its own ancestors' choices against WinLane masks; the deepest lane
 // on the path gives the window's end) instead of a 5-step SALU walk: same path, fewer instructions
 // on the pop's dependent chain.
+// The trailing sift_up of the last element is fused in: it moves back down every path node whose key
+// exceeds the last element's (a suffix of the path, which is heap ordered), so the net effect is that
+// only the path nodes p_1..p_t with key <= last's move up one level and the last element takes p_t's
+// old place. The pop therefore stops in the first window holding a path node the last element does
+// not pass — no deeper window, no re-read of the path (tests/test_heap_lane_model.py models it).
 // `at_top(top)` runs as soon as the popped entry is known (after the first window read), so the
 // caller can issue the popped node's neighbour loads while the sift still runs.
 template <class AtTop>
@@ -379,7 +384,7 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
                                          AtTop&& at_top) {
   constexpr uint64_t M62 = (1ull << 62) - 1ull, EVEN = 0x5555555555555555ull;
   const uint32_t end = --len;
-  uint32_t pos = 0;
+  uint32_t pos = 0, klast = 0;
   uint64_t last = 0, top = 0;
   const uint32_t kk = 31u - (uint32_t)__builtin_clz(lane + 2u);
   const uint32_t ki = lane + 2u - (1u << kk);
@@ -395,17 +400,33 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
         at_top(last);
         return last;
       }
+      klast = hk(last);
       at_top(top);
     }
     const uint32_t key = hk(val);
     const uint32_t sib = (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     const bool ex = node < end;
     const uint64_t VL = ballot64(ex) & M62;
+    const uint64_t LE = ballot64(key <= klast);  // nodes the last element would not pass
     // left child lane (even) takes the right child when left <= right and the right exists
     const uint64_t CR = ballot64(key >= sib) & (VL >> 1) & EVEN;
     const bool on = ex & ((CR & wl.one) == wl.one) & ((CR & wl.zero) == 0ull);  // branch-free
     const uint64_t PM = ballot64(on);
     if (PM == 0ull) break;  // the hole has no child
+    const uint64_t PU = PM & LE;
+    if (PU != PM) {  // the last element lands in this window: below the deepest moving node, or at the hole
+      uint32_t tgt = pos;
+      if (PU != 0ull) {
+        const uint32_t lu = 63u - (uint32_t)__builtin_clzll(PU);
+        const uint32_t d = 31u - (uint32_t)__builtin_clz(lu + 2u);
+        tgt = ((pos + 1u) << d) - 1u + (lu + 2u - (1u << d));
+      }
+      wave_order();
+      if ((PU >> lane) & 1ull) Hp[(node - 1u) >> 1] = val;  // lanes >= 62 are never on the path
+      if (lane == 63u) Hp[tgt] = last;
+      wave_order();
+      return top;
+    }
     const uint32_t lt = 63u - (uint32_t)__builtin_clzll(PM);  // deepest node on the path
     const uint32_t d = 31u - (uint32_t)__builtin_clz(lt + 2u), idx = lt + 2u - (1u << d);
     wave_order();
@@ -414,7 +435,10 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
     pos = ((pos + 1u) << d) - 1u + idx;
     if (d < 5) break;
   }
-  wsift_up(Hp, pos, last, lane);
+  // every path node moved up (the last element passes none of them): it fills the bottom hole
+  wave_order();
+  if (lane == 63u) Hp[pos] = last;
+  wave_order();
   return top;
 }
 

@@ -79,7 +79,7 @@ struct Tunables {
   bool avoid_xcc = true;          // TSW_WORKER_AVOID_XCD=0: coop workers also run on the planner's XCD
   bool chain_preempt = true;      // TSW_CHAIN_PREEMPT=0: chain workers finish a chain before serving queued pairs
   int worker_gs = -1;             // TSW_WORKER_GS: coop workers' g-score placement (0 global, 1 LDS u32, 2 LDS bytes)
-  int worker_fb = -1;             // TSW_WORKER_FB=0: global-g-score workers without the staged free bitmap (more waves per CU)
+  int worker_fb = -1;             // TSW_WORKER_FB=0 / 1: global-g-score workers without / with the staged free bitmap (-1: by waves per CU)
   bool dag_exit = true;           // TSW_DAG_EXIT=0: coop workers' A* runs to the goal's pop (no DAG early exit)
   uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)

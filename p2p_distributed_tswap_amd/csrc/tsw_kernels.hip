@@ -810,11 +810,16 @@ WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_
   // grids whose byte g-scores fit LDS (<= 120k cells): with many agents, trade the LDS g-scores for
   // 3x the waves (global u32 slots, L2-resident at this size)
   if (m != 0u && n_agents > 2000u && c.waves < 3u * (uint32_t)num_cu) c = make(0u, true);
-  // larger grids keep one wave per CU with the bitmap in LDS: their 4 MB g-score slots would not
-  // stay cache-resident with more waves, and the traffic slows the planner itself (C5: 3x)
   if (c.hcap < 64u) c = make(0u, false);
-  // A/B (TSW_WORKER_FB=0): global g-score grids without the staged bitmap, several waves per CU
-  if (force_fb == 0 && m == 0u) c = make(0u, false);
+  // global g-score workers: the staged free bitmap saves one L2 read per relaxation but costs LDS; drop
+  // it when that at least doubles the waves per CU (C5's 128 KiB bitmap left one wave per CU: plan
+  // 8.6 s with 255 workers, 3.97 s with 910 without it, planner sections unchanged — round 4,
+  // profiles/r4/c5_workers_ab.jsonl; round 3 measured the opposite in exit mode, before the coop
+  // workers stopped with the planner). TSW_WORKER_FB=0 / 1 forces either.
+  if (c.gs_lds == 0u && c.stage_fb != 0u && force_fb != 1) {
+    const WorkerCfg nf = make(0u, false);
+    if (nf.hcap >= 64u && (force_fb == 0 || nf.waves >= 2u * c.waves)) c = nf;
+  }
   return c;
 }
 
