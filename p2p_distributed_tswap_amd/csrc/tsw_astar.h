@@ -442,6 +442,77 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
   return top;
 }
 
+// ----------------------------------------------------------------------------
+// Register-resident heap (round 4). A* heaps are small — on C3 the heap holds 31 entries at the median
+// pop, 49 at p90 — so a heap of <= REG_HEAP_MAX = 63 entries lives in one 64-bit VGPR pair across the
+// wave in the first pop window's own layout: node 0 (the root) in lane 63, node n in 1..62 in lane n - 1
+// (siblings are lane pairs (2i, 2i + 1); lane 62 holds nothing). A pop is then the window's path test
+// with no LDS read, and values move along a path with one ds_bpermute (pull from the chosen child; for a
+// push, from the parent) instead of an LDS write / read round trip. The heap spills to the LDS array
+// when a push would pass 63 entries and is reloaded once a pop leaves <= REG_HEAP_RELOAD; both forms
+// hold the same BinaryHeap array, so the pop order is unchanged (tests/test_heap_lane_model.py models
+// rpop / rpush with the spill and reload against the restated BinaryHeap).
+// ----------------------------------------------------------------------------
+constexpr uint32_t REG_HEAP_MAX = 63u, REG_HEAP_RELOAD = 40u, REG_NONE = 0xFFFFu;
+struct RegLane {
+  uint32_t node, depth, plane, src_child;  // src_child: lane of the left child (node <= 30), else 63
+};
+__device__ __forceinline__ uint32_t reg_lane_of(uint32_t n) { return n == 0u ? 63u : n - 1u; }
+__device__ __forceinline__ RegLane reg_lane(uint32_t lane) {
+  RegLane r;
+  r.node = lane == 63u ? 0u : (lane == 62u ? REG_NONE : lane + 1u);
+  r.depth = r.node == REG_NONE ? 15u : 31u - (uint32_t)__builtin_clz(r.node + 1u);
+  r.plane = (r.node == 0u || r.node == REG_NONE) ? lane : reg_lane_of((r.node - 1u) >> 1);
+  r.src_child = (r.node != REG_NONE && r.node <= 30u) ? reg_lane_of(2u * r.node + 1u) : 63u;
+  return r;
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t x, uint32_t src) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// BinaryHeap::pop on the register heap (1 <= len <= 63), the last element's sift_up fused as in wpop:
+// the path nodes with key <= last's move up (each path node above the landing pulls its chosen child's
+// value), the last element takes the deepest one's place (the root when none moves).
+template <class AtTop>
+__device__ __forceinline__ uint64_t rpop(uint64_t& R, uint32_t& len, uint32_t lane, const WinLane& wl,
+                                         const RegLane& rl, AtTop&& at_top) {
+  constexpr uint64_t M62 = (1ull << 62) - 1ull, EVEN = 0x5555555555555555ull;
+  const uint32_t end = --len;
+  const uint64_t top = rl64(R, 63u);
+  at_top(top);
+  if (end == 0) return top;
+  const uint64_t last = rl64(R, end - 1u);  // node end >= 1 sits in lane end - 1
+  const uint32_t klast = hk(last), key = hk(R);
+  const uint32_t sib = (uint32_t)__builtin_amdgcn_mov_dpp((int)key, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  const bool ex = rl.node < end;  // lane 62 (REG_NONE) never; lane 63 (the root) is masked below
+  const uint64_t VL = ballot64(ex) & M62;
+  const uint64_t LE = ballot64(key <= klast);
+  const uint64_t CR = ballot64(key >= sib) & (VL >> 1) & EVEN;
+  const bool on = ex & ((CR & wl.one) == wl.one) & ((CR & wl.zero) == 0ull);
+  const uint64_t PU = ballot64(on) & LE;
+  const uint32_t land = PU == 0ull ? 63u : 63u - (uint32_t)__builtin_clzll(PU);
+  const uint32_t src = rl.src_child == 63u ? 63u : rl.src_child + (uint32_t)((CR >> rl.src_child) & 1ull);
+  const uint64_t pulled = bperm64(R, src);
+  const bool recv = (PU >> src) & 1ull;  // bit 63 of PU is never set
+  R = lane == land ? last : (recv ? pulled : R);
+  return top;
+}
+
+// BinaryHeap::push (sift_up(0, len)) on the register heap, len < 63: the ancestors the element passes
+// (a suffix of its root path) pull their parent's value, the element lands at depth t.
+__device__ __forceinline__ void rpush(uint64_t& R, uint32_t& len, uint64_t e, const RegLane& rl) {
+  const uint32_t p1 = len + 1u, dp = 31u - (uint32_t)__builtin_clz(p1);
+  const uint32_t sh = rl.depth <= dp ? dp - rl.depth : 0u;
+  const bool onp = rl.depth <= dp && (p1 >> sh) == rl.node + 1u;  // the hole's root path (the hole included)
+  const uint64_t G = ballot64(onp && rl.depth < dp && hk(e) < hk(R));
+  const uint32_t t = dp - (uint32_t)__popcll(G);
+  const uint64_t pulled = bperm64(R, rl.plane);
+  R = (onp && rl.depth == t) ? e : ((onp && rl.depth > t) ? pulled : R);
+  ++len;
+}
+
 // Detour bytes of a goal's K1 table for astar_wave_par<*, *, 1>: DT[c] = (D[c] - |c - goal|_1) / 2
 // (D and the Manhattan distance share parity on a 4-grid), 255 when that is >= 255 or c is blocked /
 // unreachable. One wave; D is the slot's u16 table. Only the cells of the box [x0, x1] x [y0, y1] are
@@ -498,7 +569,8 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
                                                   uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
                                                   const uint32_t* FB, int32_t* len_out, unsigned long long* pr,
                                                   const uint8_t* DT = nullptr, const uint16_t* DG = nullptr,
-                                                  uint32_t* npop = nullptr, uint32_t dag_mask = 15u) {
+                                                  uint32_t* npop = nullptr, uint32_t dag_mask = 15u,
+                                                  uint32_t reg_max = REG_HEAP_MAX) {
   const uint32_t lane = threadIdx.x & 63u;
   unsigned long long pops = 0, c_pop = 0, c_nb = 0, c_push = 0, npush = 0, tk = 0;
   auto tick = [&](unsigned long long& acc) {
@@ -542,10 +614,15 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     dstar = DG[v];
     ee = dstar != 0xFFFFu;
   }
+  // the heap starts in registers (see rpop): the start entry at the root (lane 63); reg_max = 0 keeps
+  // it in the LDS array throughout (A/B)
+  const RegLane rl = reg_lane(lane);
+  bool reg = reg_max != 0u;
+  uint64_t R = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
   if (lane == 0) {
     if constexpr (GSM == 2) GB[v] = 0x80u;
     else GS[v] = tagw;
-    Hp[0] = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
+    if (!reg) Hp[0] = R;
   }
   wave_order();
   if constexpr (PROF) tk = __builtin_amdgcn_s_memtime();
@@ -565,7 +642,7 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     // g-score / bitmap regions are disjoint from the heap, so the sift's LDS traffic cannot alias).
     uint32_t cx = 0, cy = 0, c = 0, fx = 0, fy = 0, nc = 0, fw = 0, old = 0;
     bool inb = false;
-    const uint64_t e = wpop(Hp, len, lane, wl, [&](uint64_t t) {
+    auto at_top = [&](uint64_t t) {
       cx = (uint32_t)(t >> 16) & 0xFFFFu;
       cy = (uint32_t)t & 0x7FFu;
       c = cy * W + cx;
@@ -580,7 +657,17 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       fw = FB[cy * Ww + (inb ? drow : 0u) + (fx >> 5)];
       if constexpr (GSM == 2) old = GB[nc];
       else old = GS[nc];
-    });
+    };
+    uint64_t e;
+    if (reg) {
+      e = rpop(R, len, lane, wl, rl, at_top);
+    } else {
+      e = wpop(Hp, len, lane, wl, at_top);
+      if (reg_max != 0u && len <= REG_HEAP_RELOAD) {  // back to registers (the LDS array is the heap as it stands)
+        R = Hp[rl.node < len ? rl.node : 0u];
+        reg = true;
+      }
+    }
     tick(c_pop);
     const uint32_t labc = ((uint32_t)e >> 12) & 3u;
     const uint32_t cg = hk(e) & 0x7FFFu;
@@ -621,12 +708,21 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       *len_out = -2;
       return NH_UNKNOWN;
     }
+    if (reg && len + (uint32_t)__popcll(M) > reg_max) {  // spill the register heap to the LDS array
+      wave_order();
+      if (rl.node < len) Hp[rl.node] = R;
+      reg = false;
+    }
     wave_order();
     while (M) {
       const uint32_t d = (uint32_t)__builtin_ctzll(M);
       M &= M - 1ull;
-      wsift_up(Hp, len, rl64(ent, d), lane);
-      ++len;
+      if (reg) {
+        rpush(R, len, rl64(ent, d), rl);
+      } else {
+        wsift_up(Hp, len, rl64(ent, d), lane);
+        ++len;
+      }
       ++npush;
     }
     tick(c_push);
@@ -636,8 +732,8 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       if (ee && (pops & dag_mask) == 0u) {
         uint32_t labs = 0, glab = 4u;
         for (uint32_t j0 = 0; j0 < len; j0 += 64u) {
-          const uint32_t j = j0 + lane;
-          const uint64_t en = Hp[j < len ? j : 0u];
+          const uint32_t j = reg ? rl.node : j0 + lane;  // a register heap is one pass (len <= 63)
+          const uint64_t en = reg ? R : Hp[j < len ? j : 0u];
           const uint32_t lo = (uint32_t)en, ex = lo >> 16, ey = lo & 0x7FFu, eg = hk(en) & 0x7FFFu;
           const uint32_t ec = ey * W + ex;
           bool d;

@@ -233,8 +233,8 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
       uint4* g4 = reinterpret_cast<uint4*>(GB);
       for (uint32_t c = lane; c < (ncell + 15u) / 16u; c += 64u) g4[c] = make_uint4(0u, 0u, 0u, 0u);
       wave_sync();
-      code = dag == 1u ? astar_wave_par<2, false, 1>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask)
-                       : astar_wave_par<2, false>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr, nullptr, nullptr, &np);
+      code = dag == 1u ? astar_wave_par<2, false, 1>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
+                       : astar_wave_par<2, false>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
     } else if (gs_lds == 1u) {
       if (epl % 1023u == 0u && epl > 0u) {
         for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
@@ -242,20 +242,20 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
       wave_sync();
       const uint32_t tag = epl % 1023u + 1u;
       ++epl;
-      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask)
-                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr, nullptr, nullptr, &np);
+      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
+                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
     } else {
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
       code = dag == 2u
-                 ? astar_wave_par<1, false, 2>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, DGt, &np, A.dag_mask)
-                 : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, nullptr, &np);
+                 ? astar_wave_par<1, false, 2>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, DGt, &np, A.dag_mask, A.reg_heap)
+                 : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
     }
     npt = np;
     if (L == -2 && gs_lds != 0u) {  // tier 2: global u32 g-scores (the staged detour bytes still apply)
       tiers += 1ull;
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
-      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask)
-                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, nullptr, &np);
+      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
+                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
       npt += np;
     }
     if (L == -2) {

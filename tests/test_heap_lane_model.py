@@ -245,3 +245,119 @@ def test_model_deep_heap():
         assert model_wpop(M, len(M))[0] == ref_pop(R)
         del M[len(R):]
     assert not M
+
+
+# ---------------------------------------------------------------- register-resident heap (round 4)
+# Heaps of <= 63 entries live in one 64-bit VGPR pair across the wave: node 0 (the root) in lane 63,
+# node n in 1..62 in lane n - 1 — the first pop window's own layout, so siblings are lane pairs
+# (2i, 2i + 1) and the path test is the same WinLane test. Values move along a path with one
+# ds_bpermute (pull from the chosen child / from the parent), not an LDS round trip.
+NONE = 0xFFFF
+
+
+def lane_of(n):
+    return 63 if n == 0 else n - 1
+
+
+def reg_lane(lane):
+    node = 0 if lane == 63 else (NONE if lane == 62 else lane + 1)
+    depth = log2(node + 1) if node != NONE else 15
+    plane = lane_of((node - 1) >> 1) if node not in (0, NONE) else lane
+    cl = lane_of(2 * node + 1) if node != NONE and node <= 30 else 63
+    return node, depth, plane, cl
+
+
+RL = [reg_lane(l) for l in range(64)]
+M62 = (1 << 62) - 1
+EVEN = 0x5555555555555555
+
+
+def ballot(pred):
+    return sum(1 << l for l in range(64) if pred(l))
+
+
+def model_rpop(R, length):
+    end = length - 1
+    top = R[63]
+    last = R[lane_of(end)]
+    if end == 0:
+        return last, 0
+    klast = key(last)
+    keys = [key(v) if v is not None else 1 << 40 for v in R]
+    sib = [keys[l ^ 1] for l in range(64)]  # DPP quad_perm [1,0,3,2]
+    ex = [RL[l][0] != NONE and RL[l][0] < end for l in range(64)]
+    VL = ballot(lambda l: ex[l]) & M62
+    LE = ballot(lambda l: keys[l] <= klast)
+    CR = ballot(lambda l: keys[l] >= sib[l]) & (VL >> 1) & EVEN
+    on = [l < 62 and ex[l] and (CR & WL[l][0]) == WL[l][0] and (CR & WL[l][1]) == 0 for l in range(64)]
+    PM = ballot(lambda l: on[l])
+    PU = PM & LE
+    land = 63 if PU == 0 else log2(PU)
+    new = list(R)
+    for l in range(64):
+        node, _, _, cl = RL[l]
+        src = cl + ((CR >> cl) & 1) if cl != 63 else 63
+        recv = (PU >> src) & 1
+        new[l] = last if l == land else (R[src] if recv else R[l])  # ds_bpermute from src
+    R[:] = new
+    return top, end
+
+
+def model_rpush(R, length, e):
+    p1 = length + 1
+    dp = log2(p1)
+    keys = [key(v) if v is not None else 1 << 40 for v in R]
+    onp = [RL[l][1] <= dp and (p1 >> (dp - RL[l][1])) == RL[l][0] + 1 for l in range(64)]
+    G = ballot(lambda l: onp[l] and RL[l][1] < dp and key(e) < keys[l])
+    t = dp - bin(G).count("1")
+    new = list(R)
+    for l in range(64):
+        if onp[l] and RL[l][1] == t:
+            new[l] = e
+        elif onp[l] and RL[l][1] > t:
+            new[l] = R[RL[l][2]]  # ds_bpermute from the parent's lane
+    R[:] = new
+    return length + 1
+
+
+def test_register_heap_matches_binary_heap():
+    """Pops and pushes on the register layout, spilling to / reloading from the array model of the LDS
+    heap at 63 / 40 entries as the kernel does."""
+    rng = random.Random(99)
+    for trial in range(200):
+        kr = rng.choice([2, 3, 6, 50])
+        Rf, H, R = [], [], [None] * 64
+        reg, n, uid = True, 0, 0
+        for op in range(rng.randrange(30, 500)):
+            if Rf and rng.random() < 0.47:
+                top_r = ref_pop(Rf)
+                if reg:
+                    top_m, n = model_rpop(R, n)
+                else:
+                    top_m, n = model_wpop(H, n)
+                    del H[n:]
+                    if n <= 40:  # reload
+                        R = [H[RL[l][0]] if RL[l][0] != NONE and RL[l][0] < n else None for l in range(64)]
+                        reg = True
+                assert top_m == top_r, (trial, op)
+            else:
+                k = rng.randrange(1, 5)
+                elems = []
+                for _ in range(k):
+                    uid += 1
+                    elems.append((rng.randrange(kr), uid))
+                for e in elems:
+                    ref_push(Rf, e)
+                if reg and n + k > 63:  # spill
+                    H = [R[lane_of(i)] for i in range(n)]
+                    reg = False
+                for e in elems:
+                    if reg:
+                        n = model_rpush(R, n, e)
+                    else:
+                        H.append(None)
+                        n += 1
+                        H[n - 1] = e
+                        ref_sift_up(H, n - 1)
+            cur = [R[lane_of(i)] for i in range(n)] if reg else H[:n]
+            assert cur == Rf, (trial, op, reg)
