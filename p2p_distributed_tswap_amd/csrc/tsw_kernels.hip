@@ -423,7 +423,11 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
   uint64_t* Hp = wsm;
   const uint32_t lane = threadIdx.x, ncell = G.ncell;
   // gs_lds: 0 = u32 g_scores in global slots, 1 = u32 in LDS, 2 = bytes in LDS (astar_one_b8)
-  uint32_t* GS = gs_lds == 1u ? reinterpret_cast<uint32_t*>(wsm + hcap) : gs_all + (uint64_t)blockIdx.x * ncell;
+  // LDS and global g-scores are separate pointers for separate calls (a run-time selected pointer is
+  // generic: flat loads on the pop's chain instead of ds_read)
+  uint32_t* const GSl = reinterpret_cast<uint32_t*>(wsm + hcap);
+  uint32_t* const GSg = gs_all + (uint64_t)blockIdx.x * ncell;
+  uint32_t* GS = gs_lds == 1u ? GSl : GSg;
   uint8_t* GB = reinterpret_cast<uint8_t*>(wsm + hcap);
   // free-cell bitmap after the heap and the LDS g_scores (wave_lds_bytes' carve)
   const uint32_t gsb = gs_lds == 1u ? ncell * 4u : gs_lds == 2u ? (ncell + 15u) / 16u * 16u : 0u;
@@ -460,11 +464,13 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long pr[5] = {0, 0, 0, 0, 0};
     if (!serial && prof) {
-      code = gs_lds == 2u ? astar_wave_par<2, true>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr)
-                          : astar_wave_par<1, true>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr);
+      code = gs_lds == 2u   ? astar_wave_par<2, true>(G, q.v, q.goal, tag, Hp, hcap, GSl, GB, FB, &L, pr)
+             : gs_lds == 1u ? astar_wave_par<1, true>(G, q.v, q.goal, tag, Hp, hcap, GSl, GB, FB, &L, pr)
+                            : astar_wave_par<1, true>(G, q.v, q.goal, tag, Hp, hcap, GSg, GB, FB, &L, pr);
     } else if (!serial) {
-      code = gs_lds == 2u ? astar_wave_par<2, false>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr)
-                          : astar_wave_par<1, false>(G, q.v, q.goal, tag, Hp, hcap, GS, GB, FB, &L, pr);
+      code = gs_lds == 2u   ? astar_wave_par<2, false>(G, q.v, q.goal, tag, Hp, hcap, GSl, GB, FB, &L, pr)
+             : gs_lds == 1u ? astar_wave_par<1, false>(G, q.v, q.goal, tag, Hp, hcap, GSl, GB, FB, &L, pr)
+                            : astar_wave_par<1, false>(G, q.v, q.goal, tag, Hp, hcap, GSg, GB, FB, &L, pr);
     }
 #ifdef TSW_DIAG
     else if (lane == 0) {  // lone-lane core (TSW_ASTAR_SERIAL A/B, diagnostic build only)
@@ -820,6 +826,8 @@ WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_
     const WorkerCfg nf = make(0u, false);
     if (nf.hcap >= 64u && (force_fb == 0 || nf.waves >= 2u * c.waves)) c = nf;
   }
+  // invariant the workers rely on (tsw_worker.h): LDS g-scores always come with the staged bitmap
+  if (c.gs_lds != 0u) c.stage_fb = 1u;
   return c;
 }
 

@@ -49,7 +49,7 @@ __device__ __forceinline__ uint32_t hw_xcc_id() {
 // Task chains (long, lowest priority) only go to workers with take_t: the others stay free for the
 // pairs the planner needs or will need soon.
 __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags,
-                                            unsigned long long idle_ticks) {
+                                            unsigned long long idle_ticks, uint32_t wid, uint32_t gate) {
   const unsigned long long t0 = wall_clock64();
   // one pass over the queues in priority order: >= 0 claimed (queue id), -1 nothing, -2 stop
   auto scan = [&]() -> int {
@@ -93,6 +93,10 @@ __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool tak
   // Idle: poll only the planner's publish count (one load) and rescan the queues when it moves, or
   // every 64 polls as a safety net. Idle waves polling every head and claim word kept a few lines of
   // the fabric hot and slowed the planner's own memory accesses (worse the more workers run).
+  // gate (mask): only the idle workers with (wid & gate) == (pub & gate) rescan at once on a publish
+  // — a rotating subset — the others at their next 64-poll safety rescan: a publish woke every idle
+  // worker into one herd of agent-scope loads and CASes on the same claim word (C3: ~950 of 1,020
+  // idle), which the round-4 queue-delay diagnostics put at ~68 us from enqueue to claim.
   uint32_t seen = w_ld(&cc->pub);
   for (;;) {
     const int r = scan();
@@ -107,7 +111,7 @@ __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool tak
       if (k < 8) __builtin_amdgcn_s_sleep(2);
       else __builtin_amdgcn_s_sleep(16);
       const uint32_t p = w_ld(&cc->pub);
-      if (p != seen || (k & 63u) == 63u) {
+      if ((p != seen && ((p ^ wid) & gate) == 0u) || (k & 63u) == 63u) {
         seen = p;
         break;
       }
@@ -174,13 +178,15 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   uint32_t* GSl = reinterpret_cast<uint32_t*>(wsm + hcap);  // gs_lds == 1
   uint8_t* GB = reinterpret_cast<uint8_t*>(wsm + hcap);      // gs_lds == 2
   const uint32_t gsb = gs_lds == 1u ? ncell * 4u : gs_lds == 2u ? (ncell + 15u) / 16u * 16u : 0u;
-  const uint32_t* FB = G.freebits;
+  // the free-cell bitmap: staged in LDS (A.stage_fb; worker_config stages it whenever the g-scores
+  // are in LDS) or read from global memory. The two are separate pointers passed to separate calls,
+  // never one pointer selected at run time: a selected pointer is generic, and its loads become flat
+  // loads (no ds_read), which sit on the A* pop's dependent chain.
+  uint32_t* const FBl = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wsm + hcap) + gsb);
+  const uint32_t* const FBg = G.freebits;
   const uint32_t nfw = G.H * G.Ww;
-  if (A.stage_fb) {
-    uint32_t* fb = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wsm + hcap) + gsb);
-    for (uint32_t t = lane; t < nfw; t += 64u) fb[t] = G.freebits[t];
-    FB = fb;
-  }
+  if (A.stage_fb)
+    for (uint32_t t = lane; t < nfw; t += 64u) FBl[t] = G.freebits[t];
   // DAG early exit (A.dag == 1): the detour bytes of the goal last staged (dt_goal) over the box
   // dt_box = x0 | x1 << 16 (dt_bx), y0 | y1 << 16 (dt_by), after the bitmap
   uint8_t* DT = reinterpret_cast<uint8_t*>(wsm + hcap) + gsb + (A.stage_fb ? (nfw * 4u + 15u) / 16u * 16u : 0u);
@@ -233,8 +239,8 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
       uint4* g4 = reinterpret_cast<uint4*>(GB);
       for (uint32_t c = lane; c < (ncell + 15u) / 16u; c += 64u) g4[c] = make_uint4(0u, 0u, 0u, 0u);
       wave_sync();
-      code = dag == 1u ? astar_wave_par<2, false, 1>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
-                       : astar_wave_par<2, false>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FB, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
+      code = dag == 1u ? astar_wave_par<2, false, 1>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FBl, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
+                       : astar_wave_par<2, false>(G, v, goal, 0u, Hp, hcap, nullptr, GB, FBl, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
     } else if (gs_lds == 1u) {
       if (epl % 1023u == 0u && epl > 0u) {
         for (uint32_t c = lane; c < ncell; c += 64u) GSl[c] = 0u;
@@ -242,20 +248,25 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
       wave_sync();
       const uint32_t tag = epl % 1023u + 1u;
       ++epl;
-      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
-                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FB, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
+      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FBl, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
+                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSl, nullptr, FBl, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
     } else {
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
-      code = dag == 2u
-                 ? astar_wave_par<1, false, 2>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, DGt, &np, A.dag_mask, A.reg_heap)
-                 : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
+      if (A.stage_fb)
+        code = dag == 2u
+                   ? astar_wave_par<1, false, 2>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBl, &L, nullptr, nullptr, DGt, &np, A.dag_mask, A.reg_heap)
+                   : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBl, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
+      else
+        code = dag == 2u
+                   ? astar_wave_par<1, false, 2>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBg, &L, nullptr, nullptr, DGt, &np, A.dag_mask, A.reg_heap)
+                   : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBg, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
     }
     npt = np;
     if (L == -2 && gs_lds != 0u) {  // tier 2: global u32 g-scores (the staged detour bytes still apply)
       tiers += 1ull;
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
-      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
-                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FB, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
+      code = dag == 1u ? astar_wave_par<1, false, 1>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBl, &L, nullptr, DT, nullptr, &np, A.dag_mask, A.reg_heap)
+                       : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBl, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
       npt += np;
     }
     if (L == -2) {
@@ -319,7 +330,7 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   for (;;) {
     int which = -1;
     uint32_t idx = 0;
-    if (lane == 0) which = worker_claim(A.cc, &idx, take_t, A.hflags, A.idle_ticks);
+    if (lane == 0) which = worker_claim(A.cc, &idx, take_t, A.hflags, A.idle_ticks, wid, A.wake_gate);
     which = __builtin_amdgcn_readfirstlane(which);
     if (which < 0) break;
     idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
