@@ -85,6 +85,8 @@ struct Tunables {
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
   uint32_t reg_heap = 63;         // TSW_ASTAR_REGHEAP: worker A* heaps up to this many entries in registers (0: LDS only)
   uint32_t wake_gate = 0;         // TSW_WAKE_GATE: log2 of the idle-worker subsets a publish rotates over (0: all wake)
+  uint32_t slow_poll = 0;         // TSW_SLOW_POLL: log2 of 1 / (fraction of idle workers polling at full rate) (0: all)
+  uint32_t slow_mult = 16;        // TSW_SLOW_MULT: the others' poll interval multiplier
   uint64_t worker_idle_us = 5000000;  // TSW_WORKER_IDLE_US: an idle coop worker exits after this long (test knob)
 
   static Tunables from_env() {
@@ -131,6 +133,8 @@ struct Tunables {
     t.stale_steps = (uint32_t)num("TSW_SPEC_STALE", 0, 1 << 20, t.stale_steps);
     t.reg_heap = (uint32_t)num("TSW_ASTAR_REGHEAP", 0, 63, t.reg_heap);
     t.wake_gate = (uint32_t)num("TSW_WAKE_GATE", 0, 8, t.wake_gate);
+    t.slow_poll = (uint32_t)num("TSW_SLOW_POLL", 0, 8, t.slow_poll);
+    t.slow_mult = (uint32_t)num("TSW_SLOW_MULT", 1, 1024, t.slow_mult);
     t.worker_idle_us = (uint64_t)num("TSW_WORKER_IDLE_US", 1, 5000000, (long)t.worker_idle_us);
 #endif
     return t;
@@ -1328,6 +1332,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.stale_steps = c->tun.stale_steps;
     W.reg_heap = c->tun.reg_heap;
     W.wake_gate = (1u << c->tun.wake_gate) - 1u;
+    W.slow_mask = (1u << c->tun.slow_poll) - 1u;
+    W.slow_mult = c->tun.slow_mult;
     W.idle_ticks = c->tun.worker_idle_us * 100ull;  // wall clock: 100 MHz
     W.dist = c->d_dist;
     W.gs_lds = wcfg.gs_lds;

@@ -49,7 +49,8 @@ __device__ __forceinline__ uint32_t hw_xcc_id() {
 // Task chains (long, lowest priority) only go to workers with take_t: the others stay free for the
 // pairs the planner needs or will need soon.
 __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags,
-                                            unsigned long long idle_ticks, uint32_t wid, uint32_t gate) {
+                                            unsigned long long idle_ticks, uint32_t wid, uint32_t gate,
+                                            uint32_t slow_mask, uint32_t slow_mult) {
   const unsigned long long t0 = wall_clock64();
   // one pass over the queues in priority order: >= 0 claimed (queue id), -1 nothing, -2 stop
   auto scan = [&]() -> int {
@@ -93,10 +94,15 @@ __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool tak
   // Idle: poll only the planner's publish count (one load) and rescan the queues when it moves, or
   // every 64 polls as a safety net. Idle waves polling every head and claim word kept a few lines of
   // the fabric hot and slowed the planner's own memory accesses (worse the more workers run).
-  // gate (mask): only the idle workers with (wid & gate) == (pub & gate) rescan at once on a publish
-  // — a rotating subset — the others at their next 64-poll safety rescan: a publish woke every idle
-  // worker into one herd of agent-scope loads and CASes on the same claim word (C3: ~950 of 1,020
-  // idle), which the round-4 queue-delay diagnostics put at ~68 us from enqueue to claim.
+  // Who polls and who answers a publish (round 4): every idle wave polling `pub` every ~0.5 us (agent
+  // scope, served past the L2) made that word a hot spot, and every publish woke all of them (C3: ~950
+  // of 1,020 idle) into one herd of loads and CASes on the claim words — ~70 us from enqueue to claim
+  // in the queue-delay diagnostics, and a slower planner. Now only the fast pollers (wid & slow_mask)
+  // == 0 poll at full rate, and of those only the rotating subset with ((wid >> fbits) ^ pub) & gate
+  // == 0 rescans at once; a slow poller (slow_mult times the interval) rescans whenever it sees a
+  // change — a trickle, not a herd — and everybody rescans every 64 polls as a safety net.
+  const bool fast = (wid & slow_mask) == 0u;
+  const uint32_t fbits = (uint32_t)__builtin_popcount(slow_mask);
   uint32_t seen = w_ld(&cc->pub);
   for (;;) {
     const int r = scan();
@@ -108,10 +114,16 @@ __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool tak
           __hip_atomic_load(&hflags[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
         return -1;
       if (wall_clock64() - t0 > idle_ticks) return -1;  // idle this long (5 s): safety exit
-      if (k < 8) __builtin_amdgcn_s_sleep(2);
-      else __builtin_amdgcn_s_sleep(16);
+      if (k < 8) {
+        __builtin_amdgcn_s_sleep(2);
+      } else {
+        // slow pollers (wid & slow_mask != 0) sleep slow_mult times longer: every idle wave polling the
+        // one `pub` word (agent scope, served past the L2) every ~0.5 us makes it a hot spot
+        const uint32_t m = fast ? 1u : slow_mult;
+        for (uint32_t r = 0; r < m; ++r) __builtin_amdgcn_s_sleep(16);
+      }
       const uint32_t p = w_ld(&cc->pub);
-      if ((p != seen && ((p ^ wid) & gate) == 0u) || (k & 63u) == 63u) {
+      if ((p != seen && (!fast || (((wid >> fbits) ^ p) & gate) == 0u)) || (k & 63u) == 63u) {
         seen = p;
         break;
       }
@@ -330,7 +342,7 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   for (;;) {
     int which = -1;
     uint32_t idx = 0;
-    if (lane == 0) which = worker_claim(A.cc, &idx, take_t, A.hflags, A.idle_ticks, wid, A.wake_gate);
+    if (lane == 0) which = worker_claim(A.cc, &idx, take_t, A.hflags, A.idle_ticks, wid, A.wake_gate, A.slow_mask, A.slow_mult);
     which = __builtin_amdgcn_readfirstlane(which);
     if (which < 0) break;
     idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
