@@ -84,9 +84,10 @@ struct Tunables {
   uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
   uint32_t reg_heap = 63;         // TSW_ASTAR_REGHEAP: worker A* heaps up to this many entries in registers (0: LDS only)
-  uint32_t wake_gate = 0;         // TSW_WAKE_GATE: log2 of the idle-worker subsets a publish rotates over (0: all wake)
-  uint32_t slow_poll = 0;         // TSW_SLOW_POLL: log2 of 1 / (fraction of idle workers polling at full rate) (0: all)
-  uint32_t slow_mult = 16;        // TSW_SLOW_MULT: the others' poll interval multiplier
+  // idle-worker polling (tsw_worker.h worker_claim; profiles/r4/poll_ab.txt: C3 371-383 -> 355 ms)
+  uint32_t wake_gate = 2;         // TSW_WAKE_GATE: log2 of the fast-poller subsets a publish rotates over (0: all)
+  uint32_t slow_poll = 4;         // TSW_SLOW_POLL: log2 of 1 / (fraction of idle workers polling at full rate) (0: all)
+  uint32_t slow_mult = 256;       // TSW_SLOW_MULT: the others' poll interval multiplier
   uint64_t worker_idle_us = 5000000;  // TSW_WORKER_IDLE_US: an idle coop worker exits after this long (test knob)
 
   static Tunables from_env() {

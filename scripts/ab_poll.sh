@@ -26,3 +26,4 @@ for cfg in $CFGS; do
   echo "$tag $(grep 'queue delay' gpurun_out/ab_poll_dbg_$tag.log | tail -1)" >> gpurun_out/ab_poll.txt
 done
 cat gpurun_out/ab_poll.txt
+grep -h "detour staging" gpurun_out/ab_poll_dbg_*.log >> gpurun_out/ab_poll.txt; tail -5 gpurun_out/ab_poll.txt
