@@ -97,24 +97,34 @@ def profiled_traffic(workload: str, kclass: str, algo_bytes_per_launch: float):
 
 def traffic_split(config: str, coop_traffic, steps: int, queries: int):
     """the coop plan dispatch carries the planner AND its K3 workers, so its PMC bytes
-    are split with the same plan profiled in exit mode (profiles/<tag>/pmc.json workload plan_exit:
-    the planner's k_plan dispatches alone, K3 as separate host-launched passes): planner bytes per
-    agent-step from there, worker bytes = the coop dispatch's bytes minus the planner's, per query."""
-    p = os.path.join(ROOT, "profiles", PROFILE_TAG, "pmc.json")
+    are split with profiles/<tag>/warm_split.json (scripts/warm_split.py): the same plan run warm in
+    one context (every next-hop code already stored: the workers only idle-poll) gives the planner's
+    bytes per agent-step; the workers' part is the cold dispatch's bytes minus that. The exit-mode
+    profile (workload plan_exit) is kept as a cross-check of K3's bytes per query; it cannot give the
+    planner's share (every exit relaunch re-stages the planner's state)."""
+    base = os.path.join(ROOT, "profiles", PROFILE_TAG)
+    out = {}
     try:
-        with open(p) as f:
-            wl = json.load(f)["workloads"][f"plan_exit:{config}"]
-        kp, k3 = wl["k_plan"], wl.get("K3", {})
-        planner_total = kp["hbm_bytes_per_launch"] * kp["launches"]
-        exit_steps = kp["agent_steps"]
+        with open(os.path.join(base, "warm_split.json")) as f:
+            ws = json.load(f)
+        if ws.get("config") == config:
+            out = {"source": os.path.relpath(os.path.join(base, "warm_split.json"), ROOT),
+                   "method": "warm vs cold plan dispatch (PMC), same instance",
+                   "planner_bytes_per_agent_step": ws["planner_bytes_per_agent_step"],
+                   "planner_algorithmic_bytes_per_agent_step": ws["planner_algorithmic_bytes_per_agent_step"],
+                   "profiled_workers_bytes_per_query": ws["workers_bytes_per_query"]}
     except (OSError, ValueError, KeyError, TypeError):
+        out = {}
+    try:
+        with open(os.path.join(base, "pmc.json")) as f:
+            k3 = json.load(f)["workloads"][f"plan_exit:{config}"].get("K3", {})
+        if "hbm_bytes_per_launch" in k3 and k3.get("queries"):
+            out["exit_mode_k3_bytes_per_query"] = round(k3["hbm_bytes_per_launch"] * k3["launches"] / k3["queries"], 1)
+    except (OSError, ValueError, KeyError, TypeError):
+        pass
+    if not out:
         return None
-    out = {"source": os.path.relpath(p, ROOT),
-           "planner_bytes_per_agent_step": round(planner_total / max(exit_steps, 1), 2),
-           "planner_algorithmic_bytes_per_agent_step": 46.0,
-           "exit_mode_k3_bytes_per_query": (round(k3["hbm_bytes_per_launch"] * k3["launches"] / max(k3["queries"], 1), 1)
-                                            if "hbm_bytes_per_launch" in k3 and k3.get("queries") else None)}
-    if coop_traffic is not None and steps and queries:
+    if coop_traffic is not None and steps and queries and "planner_bytes_per_agent_step" in out:
         planner_part = out["planner_bytes_per_agent_step"] * steps  # steps: agent-steps of one launch
         out["coop_dispatch_bytes"] = round(coop_traffic, 1)
         out["planner_part_bytes"] = round(planner_part, 1)

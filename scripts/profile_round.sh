@@ -24,3 +24,6 @@ for WL in plan plan_exit bfs; do
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/${WL}_pmc_fetch -o run -- python3 bench.py $A > $OUT/${WL}_pmc_fetch.json 2> $OUT/${WL}_pmc_fetch.err &&
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/${WL}_pmc_write -o run -- python3 bench.py $A > $OUT/${WL}_pmc_write.json 2> $OUT/${WL}_pmc_write.err || exit 1
 done
+# planner / worker traffic split of the coop dispatch (scripts/warm_split.py): cold vs warm plan
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/warm_pmc_fetch -o run -- python3 scripts/warm_plan.py --reps 1 > $OUT/warm_pmc_fetch.json 2> $OUT/warm_pmc_fetch.err &&
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/warm_pmc_write -o run -- python3 scripts/warm_plan.py --reps 1 > $OUT/warm_pmc_write.json 2> $OUT/warm_pmc_write.err || exit 1

@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     rows, starts, tasks = maps.config_instance(a.config)
-    out = {"config": a.config, "cold_ms": [], "warm_ms": [], "warm_waits": [], "cold_waits": []}
+    out = {"config": a.config, "cold_ms": [], "warm_ms": [], "warm_waits": [], "cold_waits": [],
+           "cold_queries": [], "warm_queries": []}
     with Planner(rows) as p:
         p.plan_mapd_arrays(starts, tasks, 50)
         for _ in range(a.reps):
@@ -32,11 +33,13 @@ def main():
             ref, _ = p.plan_mapd_arrays(starts, tasks, 2000)
             out["cold_ms"].append(round(1e3 * (time.perf_counter() - t0), 2))
             out["cold_waits"].append(p.stats()["coop_waits"])
+            out["cold_queries"].append(p.stats()["astar_queries"])
             p.reset_stats()
             t0 = time.perf_counter()
             rec, _ = p.plan_mapd_arrays(starts, tasks, 2000)
             out["warm_ms"].append(round(1e3 * (time.perf_counter() - t0), 2))
             out["warm_waits"].append(p.stats()["coop_waits"])
+            out["warm_queries"].append(p.stats()["astar_queries"])
             assert (rec == ref).all()
     print(json.dumps(out), flush=True)
 
