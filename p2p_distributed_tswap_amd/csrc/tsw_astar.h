@@ -567,7 +567,7 @@ __device__ __forceinline__ void stage_detour(uint8_t* DT, const uint16_t* D, uin
 // entry leaves the heap at its pop, the node's first). Every (dag_mask + 1) pops the wave scans the heap
 // (one ds_read per 64 entries plus a D gather, label ballots) after the pop's pushes: nothing is added
 // to the per-pop chain, and the stop comes at most dag_mask pops late.
-template <int GSM, bool PROF, int DAG = 0>
+template <int GSM, bool PROF, int DAG = 0, bool REG = true>
 __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag,
                                                   uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
                                                   const uint32_t* FB, int32_t* len_out, unsigned long long* pr,
@@ -618,9 +618,11 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     ee = dstar != 0xFFFFu;
   }
   // the heap starts in registers (see rpop): the start entry at the root (lane 63); reg_max = 0 keeps
-  // it in the LDS array throughout (A/B)
+  // it in the LDS array throughout (A/B). REG = false compiles the register heap out: on grids whose
+  // heaps mostly outgrow 63 entries (wh10k: 103 at the median pop) its live registers only add
+  // pressure to the LDS path (wh10k 11.3-11.5 -> 12.1 s with it compiled in, same box)
   const RegLane rl = reg_lane(lane);
-  bool reg = reg_max != 0u;
+  bool reg = REG && reg_max != 0u;
   uint64_t R = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
   if (lane == 0) {
     if constexpr (GSM == 2) GB[v] = 0x80u;
@@ -666,7 +668,7 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       e = rpop(R, len, lane, wl, rl, at_top);
     } else {
       e = wpop(Hp, len, lane, wl, at_top);
-      if (reg_max != 0u && len <= REG_HEAP_RELOAD) {  // back to registers (the LDS array is the heap as it stands)
+      if (REG && reg_max != 0u && len <= REG_HEAP_RELOAD) {  // back to registers (the LDS array is the heap as it stands)
         R = Hp[rl.node < len ? rl.node : 0u];
         reg = true;
       }

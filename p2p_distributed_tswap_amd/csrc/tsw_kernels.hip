@@ -466,11 +466,11 @@ __global__ void __launch_bounds__(64) k_astar_wave(DevGrid G, const AstarQuery* 
     if (!serial && prof) {
       code = gs_lds == 2u   ? astar_wave_par<2, true>(G, q.v, q.goal, tag, Hp, hcap, GSl, GB, FB, &L, pr)
              : gs_lds == 1u ? astar_wave_par<1, true>(G, q.v, q.goal, tag, Hp, hcap, GSl, GB, FB, &L, pr)
-                            : astar_wave_par<1, true>(G, q.v, q.goal, tag, Hp, hcap, GSg, GB, FB, &L, pr);
+                            : astar_wave_par<1, true, 0, false>(G, q.v, q.goal, tag, Hp, hcap, GSg, GB, FB, &L, pr);
     } else if (!serial) {
       code = gs_lds == 2u   ? astar_wave_par<2, false>(G, q.v, q.goal, tag, Hp, hcap, GSl, GB, FB, &L, pr)
              : gs_lds == 1u ? astar_wave_par<1, false>(G, q.v, q.goal, tag, Hp, hcap, GSl, GB, FB, &L, pr)
-                            : astar_wave_par<1, false>(G, q.v, q.goal, tag, Hp, hcap, GSg, GB, FB, &L, pr);
+                            : astar_wave_par<1, false, 0, false>(G, q.v, q.goal, tag, Hp, hcap, GSg, GB, FB, &L, pr);
     }
 #ifdef TSW_DIAG
     else if (lane == 0) {  // lone-lane core (TSW_ASTAR_SERIAL A/B, diagnostic build only)

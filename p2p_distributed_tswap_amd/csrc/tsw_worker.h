@@ -266,12 +266,12 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
       const uint32_t tag = slot_tag(GSg, ncell, ep, lane);
       if (A.stage_fb)
         code = dag == 2u
-                   ? astar_wave_par<1, false, 2>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBl, &L, nullptr, nullptr, DGt, &np, A.dag_mask, A.reg_heap)
-                   : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBl, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
+                   ? astar_wave_par<1, false, 2, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBl, &L, nullptr, nullptr, DGt, &np, A.dag_mask, A.reg_heap)
+                   : astar_wave_par<1, false, 0, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBl, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
       else
         code = dag == 2u
-                   ? astar_wave_par<1, false, 2>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBg, &L, nullptr, nullptr, DGt, &np, A.dag_mask, A.reg_heap)
-                   : astar_wave_par<1, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBg, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
+                   ? astar_wave_par<1, false, 2, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBg, &L, nullptr, nullptr, DGt, &np, A.dag_mask, A.reg_heap)
+                   : astar_wave_par<1, false, 0, false>(G, v, goal, tag, Hp, hcap, GSg, nullptr, FBg, &L, nullptr, nullptr, nullptr, &np, 15u, A.reg_heap);
     }
     npt = np;
     if (L == -2 && gs_lds != 0u) {  // tier 2: global u32 g-scores (the staged detour bytes still apply)
