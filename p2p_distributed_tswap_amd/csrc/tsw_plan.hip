@@ -395,6 +395,18 @@ __device__ __forceinline__ void coop_publish(const PlanArgs& P, uint32_t* s_q) {
   __hip_atomic_store(&P.cc->pub, s_q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// thread 0, while the other threads may be queueing speculative pairs: publish the needed queue's head
+// only (no needed pair is queued concurrently; the speculative head waits for the next full publish,
+// after a barrier, since a reserved speculative slot may not be written yet)
+__device__ __forceinline__ void coop_publish_needed(const PlanArgs& P, uint32_t* s_q) {
+  const uint32_t hn = min(s_q[0], P.qcap);
+  if (hn == s_q[3]) return;
+  s_q[3] = hn;
+  __hip_atomic_store(&P.cc->head_n, hn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  s_q[2] += 1u;
+  __hip_atomic_store(&P.cc->pub, s_q[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr unsigned long long COOP_NO_WORKER_TICKS = 100000ull;    // 1 ms at 100 MHz after the launch: no worker running
 constexpr unsigned long long COOP_RETRY_TICKS = 2000000ull;      // 20 ms pending: queue the pair again
 constexpr unsigned long long COOP_GIVE_UP_TICKS = 500000000ull;  // 5 s: safety valve
@@ -1036,6 +1048,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       __syncthreads();
     } else if (sec == SEC_PRE1 || sec == SEC_PRE2) {
       const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
+      // the pairs this step waits for go to the workers before the walk-ahead prefetch below: it
+      // reads up to 8 codes per agent in dependent global loads, and publishing only after it held
+      // every needed pair back ~40-60 us (round 4: the workers' enqueue -> claim delay)
+      if (P.coop && q > 0 && sec == SEC_PRE1 && P.prefetch && tid == 0) coop_publish_needed(P, s_q);
       // step start: queue every agent's next hop from the cell it is about to enter now, so
       // the assignment exit's K3 batch (if any) already carries what the movement phase reads
       if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, s_q);
