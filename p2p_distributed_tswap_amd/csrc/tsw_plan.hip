@@ -762,7 +762,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     return;
   }
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[6], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort;
+  __shared__ uint32_t s_q[6], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort;
   __shared__ uint32_t s_ap[128];  // rules: members of a rule-4 cycle rotated by the wave (<= 64), links
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
@@ -882,6 +882,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     s_ctl.status = PLAN_RUNNING;
     s_exit = 0;
     s_abort = 0;
+    s_cabort = 0;
     s_q[0] = 0;  // K3 queue of this launch (reported as qcount at every exit, DONE included)
     s_q[1] = 0;  // speculative queue (coop mode)
     s_q[2] = 0;  // publishes (coop mode)
@@ -913,6 +914,18 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
 
   for (;;) {
     if (s_exit) break;
+    if (s_cabort) {
+      // coop mode, watchdog seen at a section boundary: the position is a clean resume point, so exit
+      // as a coop give-up does and let the host finish the call in exit mode (the 1 ms watchdog test
+      // used to need the flag to land inside a wait; a section boundary is as safe)
+      if (tid == 0) {
+        s_ctl.qcount = s_q[0];
+        s_ctl.status = PLAN_NEED_QUERIES;
+        s_exit = 1;
+      }
+      __syncthreads();
+      break;
+    }
     if (s_abort) {  // watchdog: exit with the position recorded in ctl (section, cursor, rounds)
       if (tid == 0) {
         s_ctl.status = PLAN_ERROR;
@@ -924,7 +937,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     }
     const uint32_t sec = s_ctl.section;
     if (tid == 0) {
-      if (plan_abort(P)) s_abort = 1;
+      if (plan_abort(P)) {
+        if (P.coop) s_cabort = 1;
+        else s_abort = 1;
+      }
       const unsigned long long now = wall_clock64();
       s_tick[s_tsec] += now - s_tlast;
       s_tlast = now;
