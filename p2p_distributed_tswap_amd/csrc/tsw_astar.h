@@ -453,10 +453,7 @@ __device__ __forceinline__ uint64_t wpop(uint64_t* Hp, uint32_t& len, uint32_t l
 // hold the same BinaryHeap array, so the pop order is unchanged (tests/test_heap_lane_model.py models
 // rpop / rpush with the spill and reload against the restated BinaryHeap).
 // ----------------------------------------------------------------------------
-// Two levels (round 4, later): a second VGPR pair R1 holds depth 6 (node 63 + lane), so heaps of up to
-// REG_HEAP_MAX = 127 entries stay in registers (wh10k: 103 entries at the median pop); rpop2 / rpush2
-// extend the path test and the moves by that level (a depth-5 node's children are an R1 lane pair).
-constexpr uint32_t REG_HEAP_MAX = 127u, REG_HEAP_RELOAD = 100u, REG_NONE = 0xFFFFu;
+constexpr uint32_t REG_HEAP_MAX = 63u, REG_HEAP_RELOAD = 40u, REG_NONE = 0xFFFFu;
 struct RegLane {
   uint32_t node, depth, plane, src_child;  // src_child: lane of the left child (node <= 30), else 63
 };
@@ -513,61 +510,6 @@ __device__ __forceinline__ void rpush(uint64_t& R, uint32_t& len, uint64_t e, co
   const uint32_t t = dp - (uint32_t)__popcll(G);
   const uint64_t pulled = bperm64(R, rl.plane);
   R = (onp && rl.depth == t) ? e : ((onp && rl.depth > t) ? pulled : R);
-  ++len;
-}
-
-// BinaryHeap::pop on the two-level register heap, len > 63 (the last element sits in R1). As rpop, plus
-// depth 6: R1 lane i is on the path iff its parent (R0 lane 30 + i/2) is, it exists and it is the
-// parent's choice; if every R0 path node and the R1 one move up, the last element lands in R1 and the
-// depth-5 path node takes the R1 node's value (a readlane), else R1 is untouched.
-template <class AtTop>
-__device__ __forceinline__ uint64_t rpop2(uint64_t& R0, uint64_t& R1, uint32_t& len, uint32_t lane,
-                                          const WinLane& wl, const RegLane& rl, AtTop&& at_top) {
-  constexpr uint64_t M62 = (1ull << 62) - 1ull, EVEN = 0x5555555555555555ull;
-  const uint32_t end = --len;  // >= 63
-  const uint64_t top = rl64(R0, 63u);
-  at_top(top);
-  const uint64_t last = rl64(R1, end - 63u);
-  const uint32_t klast = hk(last), k0 = hk(R0), k1 = hk(R1);
-  const uint32_t s0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)k0, 0xB1, 0xF, 0xF, false);
-  const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)k1, 0xB1, 0xF, 0xF, false);
-  const bool ex0 = rl.node < end, ex1 = 63u + lane < end;
-  const uint64_t VL0 = ballot64(ex0) & M62, VL1 = ballot64(ex1);
-  const uint64_t CR0 = ballot64(k0 >= s0) & (VL0 >> 1) & EVEN;
-  const uint64_t CR1 = ballot64(k1 >= s1) & (VL1 >> 1) & EVEN;
-  const uint64_t LE0 = ballot64(k0 <= klast), LE1 = ballot64(k1 <= klast);
-  const bool on0 = ex0 & ((CR0 & wl.one) == wl.one) & ((CR0 & wl.zero) == 0ull);
-  const uint64_t PM0 = ballot64(on0);
-  const bool on1 = ex1 && ((PM0 >> (30u + (lane >> 1))) & 1ull) && ((uint32_t)((CR1 >> (lane & ~1u)) & 1ull) == (lane & 1u));
-  const uint64_t PU0 = PM0 & LE0, PU1 = ballot64(on1) & LE1;
-  const uint32_t src = rl.src_child == 63u ? 63u : rl.src_child + (uint32_t)((CR0 >> rl.src_child) & 1ull);
-  const uint64_t pulled = bperm64(R0, src);
-  const bool recv = (PU0 >> src) & 1ull;
-  if (PU0 == PM0 && PU1 != 0ull) {  // the last element lands at depth 6
-    const uint32_t i1 = (uint32_t)__builtin_ctzll(PU1), l5 = 30u + (i1 >> 1);
-    const uint64_t v1 = rl64(R1, i1);
-    R0 = lane == l5 ? v1 : (recv ? pulled : R0);
-    R1 = lane == i1 ? last : R1;
-  } else {
-    const uint32_t land = PU0 == 0ull ? 63u : 63u - (uint32_t)__builtin_clzll(PU0);
-    R0 = lane == land ? last : (recv ? pulled : R0);
-  }
-  return top;
-}
-
-// BinaryHeap::push on the two-level register heap, 63 <= len < 127: the hole is R1 lane len - 63 at
-// depth 6, its ancestors are R0 lanes.
-__device__ __forceinline__ void rpush2(uint64_t& R0, uint64_t& R1, uint32_t& len, uint64_t e, const RegLane& rl,
-                                       uint32_t lane) {
-  const uint32_t p1 = len + 1u;  // depth of the hole: 6
-  const uint32_t sh = rl.depth <= 5u ? 6u - rl.depth : 0u;
-  const bool onp = rl.depth <= 5u && (p1 >> sh) == rl.node + 1u;
-  const uint64_t G = ballot64(onp && hk(e) < hk(R0));
-  const uint32_t t = 6u - (uint32_t)__popcll(G);
-  const uint64_t pulled = bperm64(R0, rl.plane);
-  const uint64_t v5 = rl64(R0, (p1 >> 1) - 2u);  // the depth-5 ancestor (node (p1 >> 1) - 1)
-  R0 = (onp && rl.depth == t) ? e : ((onp && rl.depth > t) ? pulled : R0);
-  R1 = lane == len - 63u ? (t == 6u ? e : v5) : R1;
   ++len;
 }
 
@@ -681,7 +623,7 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
   // pressure to the LDS path (wh10k 11.3-11.5 -> 12.1 s with it compiled in, same box)
   const RegLane rl = reg_lane(lane);
   bool reg = REG && reg_max != 0u;
-  uint64_t R = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy, R1 = 0;
+  uint64_t R = ((uint64_t)(h0 << 15) << 32) | (vx << 16) | vy;
   if (lane == 0) {
     if constexpr (GSM == 2) GB[v] = 0x80u;
     else GS[v] = tagw;
@@ -723,12 +665,11 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     };
     uint64_t e;
     if (reg) {
-      e = len <= 63u ? rpop(R, len, lane, wl, rl, at_top) : rpop2(R, R1, len, lane, wl, rl, at_top);
+      e = rpop(R, len, lane, wl, rl, at_top);
     } else {
       e = wpop(Hp, len, lane, wl, at_top);
-      if (REG && reg_max != 0u && len <= min(REG_HEAP_RELOAD, reg_max - reg_max / 4u)) {  // back to registers (the LDS array is the heap as it stands)
+      if (REG && reg_max != 0u && len <= REG_HEAP_RELOAD) {  // back to registers (the LDS array is the heap as it stands)
         R = Hp[rl.node < len ? rl.node : 0u];
-        R1 = Hp[63u + lane < len ? 63u + lane : 0u];
         reg = true;
       }
     }
@@ -775,7 +716,6 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     if (reg && len + (uint32_t)__popcll(M) > reg_max) {  // spill the register heap to the LDS array
       wave_order();
       if (rl.node < len) Hp[rl.node] = R;
-      if (63u + lane < len) Hp[63u + lane] = R1;
       reg = false;
     }
     wave_order();
@@ -783,8 +723,7 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       const uint32_t d = (uint32_t)__builtin_ctzll(M);
       M &= M - 1ull;
       if (reg) {
-        if (len < 63u) rpush(R, len, rl64(ent, d), rl);
-        else rpush2(R, R1, len, rl64(ent, d), rl, lane);
+        rpush(R, len, rl64(ent, d), rl);
       } else {
         wsift_up(Hp, len, rl64(ent, d), lane);
         ++len;
@@ -797,11 +736,9 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
       // goal is among them. Off the per-pop chain: one read per 64 entries plus a D gather.
       if (ee && (pops & dag_mask) == 0u) {
         uint32_t labs = 0, glab = 4u;
-        const uint32_t nchunk = reg ? (len > 63u ? 2u : 1u) : (len + 63u) / 64u;
-        for (uint32_t ch = 0; ch < nchunk; ++ch) {
-          // a register heap is R0 (nodes 0..62), then R1 (63..126); the LDS array 64 entries a pass
-          const uint32_t j = reg ? (ch == 0u ? rl.node : 63u + lane) : ch * 64u + lane;
-          const uint64_t en = reg ? (ch == 0u ? R : R1) : Hp[j < len ? j : 0u];
+        for (uint32_t j0 = 0; j0 < len; j0 += 64u) {
+          const uint32_t j = reg ? rl.node : j0 + lane;  // a register heap is one pass (len <= 63)
+          const uint64_t en = reg ? R : Hp[j < len ? j : 0u];
           const uint32_t lo = (uint32_t)en, ex = lo >> 16, ey = lo & 0x7FFu, eg = hk(en) & 0x7FFFu;
           const uint32_t ec = ey * W + ex;
           bool d;

@@ -83,7 +83,7 @@ struct Tunables {
   bool dag_exit = true;           // TSW_DAG_EXIT=0: coop workers' A* runs to the goal's pop (no DAG early exit)
   uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
-  uint32_t reg_heap = 127;        // TSW_ASTAR_REGHEAP: worker A* heaps up to this many entries in registers (0: LDS only)
+  uint32_t reg_heap = 63;         // TSW_ASTAR_REGHEAP: worker A* heaps up to this many entries in registers (0: LDS only)
   // idle-worker polling (tsw_worker.h worker_claim; profiles/r4/poll_ab.txt: C3 371-383 -> 355 ms)
   uint32_t wake_gate = 2;         // TSW_WAKE_GATE: log2 of the fast-poller subsets a publish rotates over (0: all)
   uint32_t slow_poll = 4;         // TSW_SLOW_POLL: log2 of 1 / (fraction of idle workers polling at full rate) (0: all)
@@ -132,7 +132,7 @@ struct Tunables {
     t.dag_exit = num("TSW_DAG_EXIT", 0, 1, 1) != 0;
     t.dag_mask = (uint32_t)num("TSW_DAG_MASK", 0, 0x7FFFFFFF, t.dag_mask);
     t.stale_steps = (uint32_t)num("TSW_SPEC_STALE", 0, 1 << 20, t.stale_steps);
-    t.reg_heap = (uint32_t)num("TSW_ASTAR_REGHEAP", 0, 127, t.reg_heap);
+    t.reg_heap = (uint32_t)num("TSW_ASTAR_REGHEAP", 0, 63, t.reg_heap);
     t.wake_gate = (uint32_t)num("TSW_WAKE_GATE", 0, 8, t.wake_gate);
     t.slow_poll = (uint32_t)num("TSW_SLOW_POLL", 0, 8, t.slow_poll);
     t.slow_mult = (uint32_t)num("TSW_SLOW_MULT", 1, 1024, t.slow_mult);

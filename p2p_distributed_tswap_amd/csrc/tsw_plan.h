@@ -140,7 +140,7 @@ struct WorkerArgs {
   const uint16_t* dist;  // K1 tables, nstride entries per goal slot
   uint32_t dag_mask;     // the DAG test runs when (pops & dag_mask) == 0
   uint32_t stale_steps;  // speculative entries queued more than this many timesteps ago are dropped (0: never)
-  uint32_t reg_heap;     // A* heaps up to this many entries live in registers (0: LDS array only; <= 127)
+  uint32_t reg_heap;     // A* heaps up to this many entries live in registers (0: LDS array only; <= 63)
   uint32_t wake_gate;    // idle workers with (wid & wake_gate) == (pub & wake_gate) rescan at once on a publish
   uint32_t slow_mask, slow_mult;  // idle workers with (wid & slow_mask) != 0 poll slow_mult times less often
   unsigned long long idle_ticks;  // a worker idle this long (100 MHz ticks) exits (5 s)

@@ -361,97 +361,3 @@ def test_register_heap_matches_binary_heap():
                         ref_sift_up(H, n - 1)
             cur = [R[lane_of(i)] for i in range(n)] if reg else H[:n]
             assert cur == Rf, (trial, op, reg)
-
-
-# ---------------------------------------------------------------- two-level register heap (<= 127 entries)
-# R0 as above (nodes 0..62); R1 lane i holds node 63 + i (depth 6). Node n5 at depth 5 (31..62, lane
-# n5 - 1 of R0) has its children in R1 lanes 2 (n5 - 31) and 2 (n5 - 31) + 1 — a lane pair, so the DPP
-# sibling compare works in R1 too.
-def model_rpop2(R0, R1, length):
-    end = length - 1
-    top = R0[63]
-    last = R0[lane_of(end)] if end < 63 else R1[end - 63]
-    if end == 0:
-        return top, 0
-    klast = key(last)
-    k0 = [key(v) if v is not None else 1 << 40 for v in R0]
-    k1 = [key(v) if v is not None else 1 << 40 for v in R1]
-    ex0 = [RL[l][0] != NONE and RL[l][0] < end for l in range(64)]
-    ex1 = [63 + i < end for i in range(64)]
-    VL0 = ballot(lambda l: ex0[l]) & M62
-    VL1 = ballot(lambda i: ex1[i])
-    CR0 = ballot(lambda l: k0[l] >= k0[l ^ 1]) & (VL0 >> 1) & EVEN
-    CR1 = ballot(lambda i: k1[i] >= k1[i ^ 1]) & (VL1 >> 1) & EVEN
-    on0 = [l < 62 and ex0[l] and (CR0 & WL[l][0]) == WL[l][0] and (CR0 & WL[l][1]) == 0 for l in range(64)]
-    PM0 = ballot(lambda l: on0[l])
-    # depth-6 lane i is on the path iff its parent (R0 lane 30 + i // 2) is, it exists, and it is the
-    # parent's choice (CR1 bit of the pair's even lane: take the odd lane)
-    on1 = [ex1[i] and (PM0 >> (30 + i // 2)) & 1 and ((CR1 >> (i & ~1)) & 1) == (i & 1) for i in range(64)]
-    PM1 = ballot(lambda i: on1[i])
-    LE0 = ballot(lambda l: k0[l] <= klast)
-    LE1 = ballot(lambda i: k1[i] <= klast)
-    PU0, PU1 = PM0 & LE0, PM1 & LE1
-    n0, n1 = list(R0), list(R1)
-    if PU0 != PM0 or PM1 == 0 or PU1 == 0:
-        # the last element lands in R0 (at the deepest moving R0 node, or the root), R1 unchanged
-        land = 63 if PU0 == 0 else log2(PU0)
-        for l in range(64):
-            node, _, _, cl = RL[l]
-            src = cl + ((CR0 >> cl) & 1) if cl != 63 else 63
-            recv = (PU0 >> src) & 1
-            n0[l] = last if l == land else (R0[src] if recv else R0[l])
-    else:
-        # every R0 path node and the R1 one move up; the last element lands at the R1 node
-        i1 = log2(PU1)
-        l5 = 30 + i1 // 2  # its parent's R0 lane
-        for l in range(64):
-            node, _, _, cl = RL[l]
-            src = cl + ((CR0 >> cl) & 1) if cl != 63 else 63
-            recv = (PU0 >> src) & 1
-            n0[l] = R1[i1] if l == l5 else (R0[src] if recv else R0[l])
-        n1[i1] = last
-    R0[:], R1[:] = n0, n1
-    return top, end
-
-
-def model_rpush2(R0, R1, length, e):
-    if length < 63:
-        return model_rpush(R0, length, e)
-    p1 = length + 1  # hole at depth 6: R1 lane p - 63
-    dp = 6
-    k0 = [key(v) if v is not None else 1 << 40 for v in R0]
-    onp = [RL[l][1] <= 5 and (p1 >> (dp - RL[l][1])) == RL[l][0] + 1 for l in range(64)]
-    G = ballot(lambda l: onp[l] and key(e) < k0[l])
-    t = dp - bin(G).count("1")
-    n0 = list(R0)
-    hole = length - 63
-    l5 = [l for l in range(64) if onp[l] and RL[l][1] == 5][0]
-    for l in range(64):
-        if onp[l] and RL[l][1] == t:
-            n0[l] = e
-        elif onp[l] and RL[l][1] > t:
-            n0[l] = R0[RL[l][2]]
-    R1[hole] = e if t == 6 else R0[l5]
-    R0[:] = n0
-    return length + 1
-
-
-def test_register_heap2_matches_binary_heap():
-    rng = random.Random(2024)
-    for trial in range(150):
-        kr = rng.choice([2, 3, 6, 50])
-        Rf, R0, R1 = [], [None] * 64, [None] * 64
-        n, uid = 0, 0
-        for op in range(rng.randrange(50, 700)):
-            if Rf and (rng.random() < 0.42 or n + 4 > 127):
-                top_r = ref_pop(Rf)
-                top_m, n = model_rpop2(R0, R1, n)
-                assert top_m == top_r, (trial, op)
-            else:
-                for _ in range(rng.randrange(1, 5)):
-                    uid += 1
-                    e = (rng.randrange(kr), uid)
-                    ref_push(Rf, e)
-                    n = model_rpush2(R0, R1, n, e)
-            cur = [R0[lane_of(i)] if i < 63 else R1[i - 63] for i in range(n)]
-            assert cur == Rf, (trial, op)
