@@ -1,0 +1,21 @@
+#!/bin/bash
+# Same-box A/B/C: worktrees _ab_prev/ and _ab_b/ (each built in-tree) and the working tree (.),
+# interleaved: C3 bench lines, wh10k and C5 full plans, and the GPU A* parity tests of the working tree.
+set -o pipefail
+mkdir -p gpurun_out
+: > gpurun_out/ab_three.txt
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "astar or get_path or mapd_c3 or wh10k or c5 or serpentine" > gpurun_out/ab_three_tests.log 2>&1 || { tail -5 gpurun_out/ab_three_tests.log; exit 1; }
+tail -1 gpurun_out/ab_three_tests.log >> gpurun_out/ab_three.txt
+for rep in 1 2; do
+  for d in _ab_prev _ab_b .; do
+    (cd $d && timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu --no-bfs --no-sharded) > gpurun_out/ab3_c3.json 2>/dev/null || exit 1
+    python -c "import json; b=json.loads([l for l in open('gpurun_out/ab3_c3.json') if l.startswith('{')][-1]); print('c3 $d', b['ms_per_step'], round(b['kernel_stats']['coop_wait_ms']/3,1))" >> gpurun_out/ab_three.txt
+  done
+done
+for inst in wh10k c5; do
+  for d in _ab_prev _ab_b .; do
+    (cd $d && timeout -k 10 200 python -u scripts/scale_bench.py $inst --cpu-steps 1) > gpurun_out/ab3.jsonl 2>/dev/null || exit 1
+    python -c "import json; d=json.loads(open('gpurun_out/ab3.jsonl').read().strip().splitlines()[-1]); print('$inst $d', d['gpu_end_to_end_s'], d['coop_wait_ms'], d['prefix_bit_exact'])" >> gpurun_out/ab_three.txt
+  done
+done
+cat gpurun_out/ab_three.txt
