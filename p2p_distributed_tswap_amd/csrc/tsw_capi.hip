@@ -500,9 +500,13 @@ int ensure_astar_scratch(tsw_ctx* c) {
   const uint64_t ncell = c->G.ncell;
   c->hcap = (uint32_t)std::min<uint64_t>(4ull * ncell + 8ull, 1ull << 16);
   const uint64_t per_slot = (uint64_t)c->hcap * 8ull + ncell * 4ull;
-  const uint64_t budget = 4ull << 30;
+  // one slot (global g-scores + overflow heap) per K3 wave: a coop dispatch has at most 16 worker waves
+  // on each of the other CUs, so 4,096 slots cover every worker. A 4 GB budget capped C5's 2^20-cell
+  // slots (4.5 MB each) at 910 workers whatever the LDS allowed; 20 GB of the 288 GB lets C5 run as
+  // many workers as its LDS carve fits (round 4)
+  const uint64_t budget = 20ull << 30;
   uint64_t ns = budget / per_slot;
-  ns = std::max<uint64_t>(64, std::min<uint64_t>(ns, 16384));
+  ns = std::max<uint64_t>(64, std::min<uint64_t>(ns, 4096));
   c->nslots = (uint32_t)ns;
   HIPCHK(hipMalloc(&c->d_heaps, (size_t)ns * c->hcap * 8ull));
   HIPCHK(hipMalloc(&c->d_gs, (size_t)ns * ncell * 4ull));

@@ -826,6 +826,15 @@ WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_
     const WorkerCfg nf = make(0u, false);
     if (nf.hcap >= 64u && (force_fb == 0 || nf.waves >= 2u * c.waves)) c = nf;
   }
+  // heap-only workers (the bitmap-less global-g-score case, C5's 2^20 cells): a 2,048-entry LDS heap
+  // doubles the waves per CU — C5 3.64-3.67 s with 1,020 workers -> 3.44-3.51 s with 2,295, no query
+  // outgrowing it (profiles/r4/c5_slots_ab.txt); a larger heap would go to the global tier-3 heap
+  if (c.gs_lds == 0u && c.stage_fb == 0u && hcap_want == 0u && c.hcap > 2048u) {
+    const uint32_t h = 2048u;
+    c.hcap = h;
+    c.lds = (size_t)h * 8u;
+    c.waves = (uint32_t)num_cu * (uint32_t)std::min<size_t>(16u, WAVE_LDS_MAX / c.lds);
+  }
   // invariant the workers rely on (tsw_worker.h): LDS g-scores always come with the staged bitmap
   if (c.gs_lds != 0u) c.stage_fb = 1u;
   return c;
