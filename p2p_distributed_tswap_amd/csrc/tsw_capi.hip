@@ -85,6 +85,7 @@ struct Tunables {
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
   uint32_t reg_heap = 63;         // TSW_ASTAR_REGHEAP: worker A* heaps up to this many entries in registers (0: LDS only)
   // idle-worker polling (tsw_worker.h worker_claim; profiles/r4/poll_ab.txt: C3 371-383 -> 355 ms)
+  int chain_mask = -1;            // TSW_CHAIN_MASK: workers with (wid & mask) == mask walk task chains (-1: by agent count)
   uint32_t wake_gate = 2;         // TSW_WAKE_GATE: log2 of the fast-poller subsets a publish rotates over (0: all)
   uint32_t slow_poll = 4;         // TSW_SLOW_POLL: log2 of 1 / (fraction of idle workers polling at full rate) (0: all)
   uint32_t slow_mult = 256;       // TSW_SLOW_MULT: the others' poll interval multiplier
@@ -134,6 +135,7 @@ struct Tunables {
     t.stale_steps = (uint32_t)num("TSW_SPEC_STALE", 0, 1 << 20, t.stale_steps);
     t.reg_heap = (uint32_t)num("TSW_ASTAR_REGHEAP", 0, 63, t.reg_heap);
     t.wake_gate = (uint32_t)num("TSW_WAKE_GATE", 0, 8, t.wake_gate);
+    t.chain_mask = (int)num("TSW_CHAIN_MASK", -1, 15, -1);
     t.slow_poll = (uint32_t)num("TSW_SLOW_POLL", 0, 8, t.slow_poll);
     t.slow_mult = (uint32_t)num("TSW_SLOW_MULT", 1, 1024, t.slow_mult);
     t.worker_idle_us = (uint64_t)num("TSW_WORKER_IDLE_US", 1, 5000000, (long)t.worker_idle_us);
@@ -1318,9 +1320,11 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.QT = c->d_QT;
     W.nh = c->d_nh;
     W.nstride = c->tstride;
-    // task chains take half the workers at most (a quarter with many agents: their needed bursts
-    // are larger), the rest stay free for the pairs the planner waits on
-    W.tmask = P.n > 2000u ? 3u : 1u;
+    // every worker may walk task chains: a chain worker serves queued needed / speculative pairs
+    // between hops (W.preempt), so chains only use otherwise idle time. Round 4 A/B (chain share 1/4
+    // -> all, profiles/r4/chain_share_ab.txt): wh10k 11.58 -> 10.25 s, C5 3.33 -> 2.76 s, C3 unchanged
+    // (it was a quarter with many agents, a half otherwise)
+    W.tmask = c->tun.chain_mask >= 0 ? (uint32_t)c->tun.chain_mask : 0u;
     W.preempt = c->tun.chain_preempt ? 1u : 0u;
     W.avoid_xcc = c->tun.avoid_xcc ? 1u : 0u;
     W.hflags = c->d_flags;
