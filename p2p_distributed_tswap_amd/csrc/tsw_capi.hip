@@ -85,7 +85,7 @@ struct Tunables {
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
   uint32_t reg_heap = 63;         // TSW_ASTAR_REGHEAP: worker A* heaps up to this many entries in registers (0: LDS only)
   // idle-worker polling (tsw_worker.h worker_claim; profiles/r4/poll_ab.txt: C3 371-383 -> 355 ms)
-  int chain_mask = -1;            // TSW_CHAIN_MASK: workers with (wid & mask) == mask walk task chains (-1: by agent count)
+  int chain_mask = -1;            // TSW_CHAIN_MASK: workers with (wid & mask) == mask walk task chains (-1: all)
   uint32_t wake_gate = 2;         // TSW_WAKE_GATE: log2 of the fast-poller subsets a publish rotates over (0: all)
   uint32_t slow_poll = 4;         // TSW_SLOW_POLL: log2 of 1 / (fraction of idle workers polling at full rate) (0: all)
   uint32_t slow_mult = 256;       // TSW_SLOW_MULT: the others' poll interval multiplier
