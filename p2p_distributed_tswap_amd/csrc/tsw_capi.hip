@@ -67,6 +67,7 @@ struct Tunables {
   bool prefetch = true;           // TSW_NO_PREFETCH: no speculative next-hop prefetch
   uint32_t wave_rules_max = 0xFFFFFFFFu;  // TSW_WAVE_RULES_MAX: wave-0 rules rounds when n <= this
   uint32_t wide_prefetch = 8;     // TSW_WIDE_PREFETCH: resolved hops walked ahead (0 = candidates only)
+  uint32_t wide_hi = 16, wide_lo = 4;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops with a small / large speculative backlog
   uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
   uint32_t prefetch_ext = 7;      // TSW_PREFETCH_EXT: bit 0 DAG from an agent's own unresolved cell, bit 1 walk past the pickup, bit 2 walk-ahead for agents a firing changed (C3 476 -> 409 ms with bits 0-1)
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
@@ -117,6 +118,8 @@ struct Tunables {
     t.prefetch = getenv("TSW_NO_PREFETCH") == nullptr;
     t.wave_rules_max = (uint32_t)num("TSW_WAVE_RULES_MAX", 0, 0xFFFFFFFFl, t.wave_rules_max);
     t.wide_prefetch = (uint32_t)num("TSW_WIDE_PREFETCH", 0, 1 << 16, t.wide_prefetch);
+    t.wide_hi = (uint32_t)num("TSW_WIDE_HI", 0, 1 << 16, t.wide_hi);
+    t.wide_lo = (uint32_t)num("TSW_WIDE_LO", 1, 1 << 16, t.wide_lo);
     t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 16, t.dag_prefetch);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
@@ -1208,6 +1211,9 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   // TSW_WAVE_RULES_MAX caps n for A/B
   P.wave_rules_max = c->tun.wave_rules_max;
   P.wide_prefetch = c->tun.wide_prefetch;
+  P.wide_hi = c->tun.wide_hi ? c->tun.wide_hi : c->tun.wide_prefetch;
+  P.wide_lo = c->tun.wide_lo;
+  P.spec_hi = 0;  // set per launch from the worker count (run_plan_impl)
   P.dag_prefetch = c->tun.dag_prefetch;
   P.prefetch_ext = c->tun.prefetch_ext;
   P.dist = c->d_dist;
@@ -1354,6 +1360,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.wpb = W.lds_per_wave ? (uint32_t)std::min<size_t>(block / 64u, lds / W.lds_per_wave) : 0u;
     const uint32_t want = W.wpb * (uint32_t)std::max(c->num_cu - 1, 0);
     W.nworkers = std::min(want, c->nslots);
+    P.spec_hi = 2u * W.nworkers;  // a backlog of two pairs per worker counts as keeping up
     wblocks = W.wpb ? (W.nworkers + W.wpb - 1u) / W.wpb : 0u;
     if (c->tun.plan_debug)
       fprintf(stderr, "[k_plan] workers: %u waves (%u per workgroup), g-scores %u, heap %u entries, DAG exit %u, %u B LDS each\n",

@@ -51,6 +51,8 @@ struct PlanArgs {
   uint32_t part_lds;            // !agents_lds: PART_* agent arrays carved in LDS anyway (flat accesses)
   uint32_t wave_rules_max;      // rules rounds run in wave 0 alone when n <= this
   uint32_t wide_prefetch;       // 0: off; else also (succ cell, goal) of every agent, path walked this many hops ahead
+  uint32_t wide_hi, wide_lo;    // coop mode: step-start walk-ahead hops when the speculative backlog is small / large
+  uint32_t spec_hi;             // coop mode: backlog (queued, unclaimed speculative pairs) counted as small up to this
   uint32_t dag_prefetch;        // walk-ahead also queues the shortest-path successors of the first unresolved cell
   uint32_t prefetch_ext;        // bit 0: DAG from an agent's own unresolved cell; bit 1: walk on past the pickup
   const uint16_t* dist;         // K1 distance tables (nstride entries per slot), for dag_prefetch

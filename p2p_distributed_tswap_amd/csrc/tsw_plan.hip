@@ -650,8 +650,8 @@ __device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, 
 //    (prefetch_ext bit 0);
 //  * an agent heading to a pickup whose walk reaches it continues along the delivery leg: the
 //    state machine switches its goal there (tswap.rs:113-118) (prefetch_ext bit 1).
-__device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
-  const uint32_t tid = threadIdx.x, bd = blockDim.x, hops = P.wide_prefetch ? P.wide_prefetch : 1u;
+__device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t hops) {
+  const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (spec_full(P, s_q)) break;
     // heading to a pickup: the pair the state machine needs on arrival (goal := delivery,
@@ -762,7 +762,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     return;
   }
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[6], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort;
+  __shared__ uint32_t s_q[6], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort, s_hops;
   __shared__ uint32_t s_ap[128];  // rules: members of a rule-4 cycle rotated by the wave (<= 64), links
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
@@ -1063,6 +1063,22 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       }
       __syncthreads();
     } else if (sec == SEC_PRE1 || sec == SEC_PRE2) {
+      if (sec == SEC_PRE1 && tid == 0) {
+        // walk-ahead depth (coop): 16 hops on grids up to 2^18 cells while the workers keep up with the
+        // speculative queue (8 when it backs up), 4 on larger grids, where every hop is a miss into a
+        // 1 MB-stride code store (round 4 A/Bs, profiles/r4/spec_depth_ab.txt: 16 hops wh10k 10.25 ->
+        // 9.68 s, C3 -1.6 %; C5 2.75 -> 3.16 s at 16 hops, 2.60 s at 4)
+        uint32_t h = P.wide_prefetch ? P.wide_prefetch : 1u;
+        if (P.coop && P.wide_prefetch && P.spec_hi) {
+          if (P.ncell > (1u << 18)) {
+            h = P.wide_lo;
+          } else {
+            const uint32_t hs = min(s_q[1], P.qscap), cs = ld_agent(&P.cc->claim_s);
+            h = (hs > cs ? hs - cs : 0u) <= P.spec_hi ? P.wide_hi : h;
+          }
+        }
+        s_hops = h;
+      }
       const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
       // the pairs this step waits for go to the workers before the walk-ahead prefetch below: it
       // reads up to 8 codes per agent in dependent global loads, and publishing only after it held
@@ -1070,7 +1086,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       if (P.coop && q > 0 && sec == SEC_PRE1 && P.prefetch && tid == 0) coop_publish_needed(P, s_q);
       // step start: queue every agent's next hop from the cell it is about to enter now, so
       // the assignment exit's K3 batch (if any) already carries what the movement phase reads
-      if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, s_q);
+      if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, s_q, s_hops);
       if (P.coop && tid == 0) {  // speculative pairs start resolving now
         const unsigned long long t0 = P.dbg ? wall_clock64() : 0ull;
         coop_publish(P, s_q);
