@@ -4,8 +4,10 @@ Contract (driver): python bench.py --gpus N --steps K --warmup W ; for N > 1 it 
 launched under torch.distributed.run, one rank per GPU. Rank 0 prints ONE JSON line.
 
 Workload: BASELINE.json configs[2], the largest single-GPU planning config — warehouse-like
-170x84 grid (shelf blocks, 1-wide aisles, seed 0x170084), 1,000 agents, 3,000-task MAPD stream,
-reference step cap (timestep > 2000). One bench "step" = one complete tsw_plan_mapd over that
+170x84 grid (shelf blocks, 1-wide aisles, seed 0x170084), 1,000 agents, a well-formed 32,000-task
+MAPD stream (task endpoints disjoint from the agents' start cells, maps.make_wf_instance; the
+stream outlasts the horizon, so every one of the 2,001 timesteps moves agents — the round-1..4
+instance froze from t = 446), reference step cap (timestep > 2000). One bench "step" = one complete tsw_plan_mapd over that
 instance from an empty table store: K1 BFS tables for every goal cell, next-hop resolution (K3
 exact A*), then every timestep's K4 assign -> K2 step -> record on the device. The instance
 (a few KB of host arrays) is handed over through the C ABI like the reference's
@@ -17,7 +19,8 @@ Extra objects on the line:
   roofline      the kernel class with the most device time inside the timed steps (HIP events
                 on the library's stream, tsw_get_stats), algorithmic bytes per launch, and the
                 PMC traffic per launch from profiles/<PROFILE_TAG>/pmc.json — only when that file
-                was measured on THIS workload (same algorithmic bytes per launch), else null. The
+                was measured on THIS workload (same algorithmic bytes per launch) with THIS build
+                (its build_id equals the loaded library's tsw_build_id), else null. The
                 plan dispatch (k_plan) carries the planner AND its exact-A* workers (coop mode): its
                 algorithmic bytes are 46 B per agent-step plus 17 B per worker query.
   latency       k_plan against its latency floor (bound "latency"): rules / movement rounds x the
@@ -48,7 +51,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md ("HBM: 8 TB/s peak")
-PROFILE_TAG = "r4"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
+PROFILE_TAG = "r5"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
 BFS_WORKLOAD = "bfs:den520d_10k"
 
 
@@ -77,17 +80,29 @@ def parse():
     return ap.parse_args()
 
 
-def profiled_traffic(workload: str, kclass: str, algo_bytes_per_launch: float):
+def running_build_id(diag: bool = False):
+    try:
+        from p2p_distributed_tswap_amd import build_id
+        return build_id(diag)
+    except Exception:  # noqa: BLE001 — no library: nothing can be paired with a profile
+        return None
+
+
+def profiled_traffic(workload: str, kclass: str, algo_bytes_per_launch: float, build: str = None):
     """HBM bytes per launch of kernel class `kclass` measured by PMC on `workload`
     (profiles/<PROFILE_TAG>/pmc.json, written by scripts/summarize_profile.py from separate
     FETCH_SIZE / WRITE_SIZE passes with the gfx950 FETCH_SIZE x2 correction). Returned only if the
-    profiled run had the same algorithmic bytes per launch (within 2 %): a profile of another
-    workload never feeds this line."""
+    profiled run had the same algorithmic bytes per launch (within 2 %) AND was recorded with the
+    library build that is running now (pmc.json `build_id` == tsw_build_id): a profile
+    of another workload or of other code never feeds this line."""
     p = os.path.join(ROOT, "profiles", PROFILE_TAG, "pmc.json")
     try:
         with open(p) as f:
-            d = json.load(f)["workloads"][workload][kclass]
+            pj = json.load(f)
+        d = pj["workloads"][workload][kclass]
     except (OSError, ValueError, KeyError):
+        return None, None
+    if build is None or pj.get("build_id") != build:
         return None, None
     a = float(d.get("algorithmic_bytes_per_launch", 0.0))
     if a <= 0 or abs(a - algo_bytes_per_launch) > 0.02 * algo_bytes_per_launch or "hbm_bytes_per_launch" not in d:
@@ -95,7 +110,7 @@ def profiled_traffic(workload: str, kclass: str, algo_bytes_per_launch: float):
     return float(d["hbm_bytes_per_launch"]), os.path.relpath(p, ROOT)
 
 
-def traffic_split(config: str, coop_traffic, steps: int, queries: int):
+def traffic_split(config: str, coop_traffic, steps: int, queries: int, build: str = None):
     """the coop plan dispatch carries the planner AND its K3 workers, so its PMC bytes
     are split with profiles/<tag>/warm_split.json (scripts/warm_split.py): the same plan run warm in
     one context (every next-hop code already stored: the workers only idle-poll) gives the planner's
@@ -107,7 +122,7 @@ def traffic_split(config: str, coop_traffic, steps: int, queries: int):
     try:
         with open(os.path.join(base, "warm_split.json")) as f:
             ws = json.load(f)
-        if ws.get("config") == config:
+        if ws.get("config") == config and build is not None and ws.get("build_id") == build:
             out = {"source": os.path.relpath(os.path.join(base, "warm_split.json"), ROOT),
                    "method": "warm vs cold plan dispatch (PMC), same instance",
                    "planner_bytes_per_agent_step": ws["planner_bytes_per_agent_step"],
@@ -288,7 +303,7 @@ def sharded_plan_leg(args, rank, world, dev, dist, barrier, allmax):
     if rank != 0:
         return None
     return {
-        "instance": "c5_sortation_1024_10k (BASELINE configs[4]): 1024x1024, 10,000 agents, 10,000 tasks, cap 2000",
+        "instance": "c5_sortation_1024_10k (BASELINE configs[4]): 1024x1024, 10,000 agents, well-formed 24,000-task stream, cap 2000",
         "k3": f"per-step batches sharded by goal owner (goal % {world}) over {args.dist_backend}, all-reduce(MIN) of u8 codes",
         "sharded_plan_s": round(times[0], 3),
         "replica_plan_s_rank0_alone": round(replica_s, 3),
@@ -339,10 +354,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
-    fac, n_agents, n_tasks, seed = maps.CONFIGS[args.config]
-    rows = fac()
+    _, n_agents, n_tasks, _ = maps.CONFIGS[args.config]
+    rows, starts, tasks = maps.config_instance(args.config, rank)  # replicas: seed + rank
     h, w = len(rows), len(rows[0])
-    starts, tasks = maps.make_instance(rows, n_agents, n_tasks, seed + rank)
+    build = running_build_id(args.diag)
     workload = f"{'plan_exit' if args.exit_mode else 'plan'}:{args.config}"
 
     value = dt_max = None
@@ -414,7 +429,7 @@ def main():
         name, dom_ms, dom_launches, per_launch_bytes = cats[dom]
         avg_launch_ms = dom_ms / max(dom_launches, 1)
         achieved = per_launch_bytes / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-        traffic, traffic_src = profiled_traffic(workload, dom, per_launch_bytes)
+        traffic, traffic_src = profiled_traffic(workload, dom, per_launch_bytes, build)
         roofline = {
             "kernel": name,
             "bound": "hbm",
@@ -442,7 +457,7 @@ def main():
         }
         plans = max(int(st["walker_launches"]), 1) if dom == "k_plan" else max(args.steps, 1)
         roofline["traffic_split"] = (traffic_split(args.config, traffic, n_agents * steps_total / plans,
-                                                   st["astar_queries"] / plans)
+                                                   st["astar_queries"] / plans, build)
                                      if dom == "k_plan" and not args.exit_mode else None)
         latency = latency_roofline(st, us_wave, us_pass)
 
@@ -493,7 +508,8 @@ def main():
         cells_per_s = allsum(float(mine.size * ncell)) * args.bfs_reps / tbw
         k_gbs = mine.size * bytes_goal / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
         algo_launch = float(mine.size * bytes_goal)
-        btraffic, btraffic_src = profiled_traffic(BFS_WORKLOAD, "K1", algo_launch) if world == 1 else (None, None)
+        btraffic, btraffic_src = (profiled_traffic(BFS_WORKLOAD, "K1", algo_launch, build) if world == 1
+                                  else (None, None))
         bfs = {
             "workload": "den520d-like 256x257 cave (seed 0x520D), distinct goals",
             "goals_total": int(goals.size),
@@ -541,12 +557,18 @@ def main():
             "dtype": "int32",
             "data": "synthetic (seeded warehouse-like map and MAPD task stream; replicas seed+rank)",
             "config": {
-                "workload": (f"{args.config}: {w}x{h} grid, {n_agents} agents, {n_tasks}-task MAPD stream, "
-                             "cap 2000, full plan from an empty table store per step "
+                "workload": (f"{args.config}: {w}x{h} grid, {n_agents} agents, "
+                             f"{'well-formed ' if args.config in maps.WELL_FORMED else ''}{n_tasks}-task MAPD "
+                             "stream, cap 2000, full plan from an empty table store per step "
                              f"(BASELINE configs[{list(maps.CONFIGS).index(args.config)}])"),
                 "agents": n_agents, "tasks": n_tasks, "grid": f"{w}x{h}",
-                "timesteps_per_plan": Ts, "parallelism": f"replicas x{world} (step not shardable)",
+                "well_formed": args.config in maps.WELL_FORMED,
+                "timesteps_per_plan": Ts,
+                # timesteps t >= 1 of the last timed plan in which any agent moved
+                "timesteps_moving": maps.moving_timesteps(last_rec) if last_rec is not None else None,
+                "parallelism": f"replicas x{world} (step not shardable)",
             },
+            "build_id": build,
             "roofline": roofline,
             "latency": latency,
             "bfs": bfs,

@@ -61,8 +61,9 @@ extern "C" {
 /* Revision of this ABI: bumped whenever a struct or a signature changes, so a caller
  * built against an older header can refuse to run. 3: tsw_opts grew to 24 bytes (watchdog_ms),
  * tsw_next_hop_tables_device gained dev_dist; 4: tsw_abi_version, lazy task-cell checks,
- * tsw_plan_mapd_resolved / tsw_next_hop_codes. */
-#define TSW_ABI_VERSION 4
+ * tsw_plan_mapd_resolved / tsw_next_hop_codes; 5: tsw_build_id, entry points refuse re-entry from a
+ * tsw_plan_mapd_resolved resolver (TSW_EINVAL). */
+#define TSW_ABI_VERSION 5
 
 /* AgentState discriminants in declaration order (src/map/agent.rs:9-15) */
 #define TSW_PICKING 0
@@ -128,6 +129,10 @@ void tsw_destroy(tsw_ctx *ctx);
 const char *tsw_last_error(const tsw_ctx *ctx);
 /* TSW_ABI_VERSION the library was built with; compare it with the header's before tsw_create. */
 int tsw_abi_version(void);
+/* Provenance of the build: the first 8 bytes of the sha1 of the library's sources (kernels, host
+ * runtime, this header) as computed by the build, 0 if the build did not set it. Measurement tools
+ * record it beside a profile and refuse to pair a profile with a different build. */
+uint64_t tsw_build_id(void);
 
 /* Replaces `tswap_mapd(grid, initial_positions, tasks)` (tswap.rs:39-172).
  * out: caller-allocated n*(max_t+1) records, agent-major:
@@ -138,7 +143,7 @@ int tsw_abi_version(void);
  * (:136), or whose off-grid/blocked delivery is looked up when its agent reaches
  * the pickup (:112). A bad task cell that is never looked up does not fail the
  * call. The nearest-pickup choice uses the raw pickup point (:125-130), its
- * coordinates clamped to 0xFFFF (cannot change the winner: see tsw_capi.hip). */
+ * coordinates clamped to 0xFFFE (cannot change the winner: see tsw_capi.hip). */
 int tsw_plan_mapd(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const tsw_task *tasks,
                   uint32_t m, uint32_t max_t, tsw_rec *out, uint32_t *out_T);
 
@@ -156,7 +161,10 @@ int tsw_plan_mapd_trace(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const
  * itself. resolve must fill code[i] with the next-hop code of get_path(start[i], goal[i]) (0..3
  * = S,E,N,W neighbour, tswap.rs:62 order; 4 = stay), e.g. by sending each pair to the rank that
  * owns its goal (tsw_next_hop_codes there) and gathering the codes, and return 0; anything else,
- * or a code > 4, fails the call with TSW_EINVAL. The plan is bit-identical to tsw_plan_mapd's. */
+ * or a code > 4, fails the call with TSW_EINVAL. The plan is bit-identical to tsw_plan_mapd's.
+ * The resolver must not call back into `ctx` (the suspended plan owns its queues and table store):
+ * every entry point returns TSW_EINVAL on a context whose resolver is running. Answer the pairs
+ * from another context (e.g. the goal owner's, tsw_next_hop_codes there). */
 typedef int (*tsw_resolve_fn)(void *user, uint32_t k, const uint32_t *start, const uint32_t *goal, uint8_t *code);
 int tsw_plan_mapd_resolved(tsw_ctx *ctx, const tsw_point *starts, uint32_t n, const tsw_task *tasks,
                            uint32_t m, uint32_t max_t, tsw_rec *out, uint32_t *goal_out, uint32_t *out_T,

@@ -25,7 +25,7 @@ import numpy as np
 
 __all__ = [
     "AgentState", "Task", "TswapError", "Planner", "tswap_mapd", "tswap_step",
-    "load_library", "LIB_PATH", "grid_to_bytes",
+    "load_library", "LIB_PATH", "grid_to_bytes", "build_id",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -35,7 +35,7 @@ LIB_PATH = os.path.join(_HERE, "libtswap_hip.so")
 DIAG_LIB_PATH = os.path.join(_HERE, "libtswap_hip_diag.so")
 
 TSW_OK, TSW_EINVAL, TSW_ENOMEM, TSW_EHIP, TSW_EOVERFLOW = 0, -22, -12, -5, -75
-TSW_ABI_VERSION = 4  # include/tswap.h
+TSW_ABI_VERSION = 5  # include/tswap.h
 TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP, TSW_F_EXIT_MODE = 1, 2, 4
 # TswapAction (bin/decentralized/agent.rs:321-326), include/tswap.h TSW_ACT_*
 TSW_ACT_MOVE, TSW_ACT_GOAL_SWAP, TSW_ACT_ROTATION, TSW_ACT_WAIT = 0, 1, 2, 3
@@ -117,7 +117,7 @@ EXPORTED_SYMBOLS = (
     "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables", "tsw_dist_tables_device",
     "tsw_import_tables_device", "tsw_next_hop_tables", "tsw_next_hop_tables_device", "tsw_import_next_hops_device",
     "tsw_clear_tables", "tsw_get_stats", "tsw_reset_stats", "tsw_set_timing", "tsw_probe_round_floors",
-    "tsw_abi_version", "tsw_plan_mapd_resolved", "tsw_next_hop_codes",
+    "tsw_abi_version", "tsw_plan_mapd_resolved", "tsw_next_hop_codes", "tsw_build_id",
 )
 
 # tsw_resolve_fn (include/tswap.h): int (*)(void *user, uint32_t k, const uint32_t *start,
@@ -135,6 +135,16 @@ def load_library(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise TswapError(TSW_EHIP, f"HIP library not built: {path} (run __graft_entry__.build())")
     lib = ctypes.CDLL(path)
+    # the ABI revision first: an older library lacks the newer symbols, and binding them
+    # before this check would fail with a bare AttributeError instead of the rebuild message
+    abi = None
+    if hasattr(lib, "tsw_abi_version"):
+        lib.tsw_abi_version.argtypes = []
+        lib.tsw_abi_version.restype = ctypes.c_int
+        abi = lib.tsw_abi_version()
+    if abi != TSW_ABI_VERSION:
+        raise TswapError(TSW_EINVAL, f"{path}: ABI {abi}, this binding mirrors {TSW_ABI_VERSION} "
+                                     "(rebuild with __graft_entry__.build())")
     P = ctypes.POINTER
     u32, i32, u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
     vp = ctypes.c_void_p
@@ -166,11 +176,8 @@ def load_library(path: str = LIB_PATH):
     lib.tsw_plan_mapd_resolved.restype = ctypes.c_int
     lib.tsw_next_hop_codes.argtypes = [vp, P(u32), P(u32), u32, P(ctypes.c_uint8)]
     lib.tsw_next_hop_codes.restype = ctypes.c_int
-    lib.tsw_abi_version.argtypes = []
-    lib.tsw_abi_version.restype = ctypes.c_int
-    if lib.tsw_abi_version() != TSW_ABI_VERSION:
-        raise TswapError(TSW_EINVAL, f"{path}: ABI {lib.tsw_abi_version()}, this binding mirrors {TSW_ABI_VERSION} "
-                                     "(rebuild with __graft_entry__.build())")
+    lib.tsw_build_id.argtypes = []
+    lib.tsw_build_id.restype = ctypes.c_uint64
     for name in ("tsw_plan_mapd", "tsw_plan_mapd_trace", "tsw_step", "tsw_get_path_next", "tsw_decide", "tsw_dist_tables",
                  "tsw_dist_tables_device", "tsw_import_tables_device", "tsw_clear_tables", "tsw_next_hop_tables",
                  "tsw_next_hop_tables_device", "tsw_import_next_hops_device", "tsw_get_stats", "tsw_reset_stats",
@@ -178,6 +185,12 @@ def load_library(path: str = LIB_PATH):
         getattr(lib, name).restype = ctypes.c_int
     _libs[path] = lib
     return lib
+
+
+def build_id(diag: bool = False) -> str:
+    """tsw_build_id() of the loaded library as 16 hex digits: the sha1 of the sources it was built from
+    (__graft_entry__.source_hash). Profiles record it; bench.py pairs a profile only with its build."""
+    return f"{load_library(DIAG_LIB_PATH if diag else LIB_PATH).tsw_build_id():016x}"
 
 
 def grid_to_bytes(grid) -> tuple:

@@ -43,6 +43,10 @@
 
 namespace tsw {
 
+#ifdef TSW_DIAG
+// The kernel is compiled into the diagnostic build only: it is a measured null result
+// (5.5 ms vs k_bfs_blk's 2.7 ms on den520d's 10k goals) that the production path never selects.
+
 namespace {
 
 constexpr uint32_t MG_G = 16;  // goals per group (bits of the u16 visited mask)
@@ -334,5 +338,13 @@ hipError_t launch_bfs_mg(const MgBfsArgs& A, int max_lds, int num_cu, hipStream_
   hipLaunchKernelGGL(k_bfs_mg, dim3(grid), dim3(1024), lds, s, A);
   return hipGetLastError();
 }
+
+#else   // production build: no k_bfs_mg (TSW_BFS_KERNEL is a diagnostic knob)
+
+size_t bfs_mg_lds_bytes(uint32_t, uint32_t, uint32_t) { return ~(size_t)0; }
+
+hipError_t launch_bfs_mg(const MgBfsArgs&, int, int, hipStream_t) { return hipErrorInvalidValue; }
+
+#endif  // TSW_DIAG
 
 }  // namespace tsw

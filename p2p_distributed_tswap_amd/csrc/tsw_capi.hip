@@ -267,8 +267,7 @@ struct tsw_ctx {
   uint8_t* d_nhc = nullptr;
   // tasks
   size_t tcap = 0;
-  uint32_t *d_pick_xy = nullptr, *d_pick = nullptr, *d_dlv = nullptr, *d_unused = nullptr;
-  uint8_t* d_used = nullptr;
+  uint32_t *d_live = nullptr, *d_pick = nullptr, *d_dlv = nullptr, *d_unused = nullptr;
   // records
   uint64_t* d_rec = nullptr;
   size_t rec_cap = 0;
@@ -303,6 +302,19 @@ struct tsw_ctx {
     c->err = (msg);      \
     return (code);       \
   } while (0)
+
+// a tsw_plan_mapd_resolved resolver must not call back into the planning context (its
+// queue, result buffers and table store are in use by the suspended plan): every entry point that
+// touches the context refuses such a call.
+#define NOT_FROM_RESOLVER(c)                                                                         \
+  do {                                                                                               \
+    if ((c)->resolver) RET(TSW_EINVAL, "re-entrant call on a context inside its own next-hop resolver"); \
+  } while (0)
+
+// build provenance (tsw_build_id): first 16 hex digits of the sha1 of the sources, set by the build
+#ifndef TSW_SRC_HASH
+#define TSW_SRC_HASH 0ull
+#endif
 
 #define TRY(expr)            \
   do {                       \
@@ -1218,10 +1230,9 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.prefetch_ext = c->tun.prefetch_ext;
   P.dist = c->d_dist;
   P.nbmask = c->d_nbmask;
-  P.pick_xy = c->d_pick_xy;
+  P.live = c->d_live;
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;
-  P.used = c->d_used;
   P.goal_tab = c->d_goal_tab;
   P.nh = c->d_nh;
   P.nstride = c->tstride;
@@ -1552,7 +1563,8 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   if (!out_T || (n && (!starts || !out)) || (m && !tasks)) RET(TSW_EINVAL, "null argument");
   if (max_t > (1u << 20)) RET(TSW_EINVAL, "max_t too large");
   TRY(set_device(c));
-  std::vector<uint32_t> vcell(n), pick(m), dlv(m), pick_xy(m);
+  const uint32_t m4 = (m + 3u) & ~3u;  // K4 reads the live array as 16-B vectors
+  std::vector<uint32_t> vcell(n), pick(m), dlv(m), live(std::max<uint32_t>(m4, 4u), TASK_TAKEN);
   std::vector<uint32_t> goalset;
   goalset.reserve(n + 2 * (size_t)m);
   for (uint32_t i = 0; i < n; ++i) {
@@ -1564,24 +1576,24 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   // assigned (pos2id[&task.pickup], tswap.rs:136), the delivery when its agent reaches the pickup
   // (:112) — so an off-grid or blocked one fails the call only then (k_plan ERR_BAD_*), exactly
   // where the reference panics. The assignment's Manhattan distance still uses the raw point
-  // (:125-130); coordinates are clamped to 16 bits, which cannot change which task wins: any point
-  // past 0xFFFF is farther than every on-grid pickup (sides <= 2048), and assigning it fails anyway.
+  // (:125-130); coordinates are clamped to 0xFFFE (0xFFFFFFFF marks a taken task), which cannot
+  // change which task wins: any point past 0xFFFE is farther than every on-grid pickup (sides <=
+  // 2048), and assigning it fails anyway.
   for (uint32_t k = 0; k < m; ++k) {
     if (!cell_ok(c, tasks[k].pickup.x, tasks[k].pickup.y, &pick[k])) pick[k] = CELL_BAD;
     if (!cell_ok(c, tasks[k].delivery.x, tasks[k].delivery.y, &dlv[k])) dlv[k] = CELL_BAD;
-    pick_xy[k] = std::min<uint32_t>(tasks[k].pickup.x, 0xFFFFu) | (std::min<uint32_t>(tasks[k].pickup.y, 0xFFFFu) << 16);
+    live[k] = std::min<uint32_t>(tasks[k].pickup.x, 0xFFFEu) | (std::min<uint32_t>(tasks[k].pickup.y, 0xFFFEu) << 16);
     if (pick[k] != CELL_BAD) goalset.push_back(pick[k]);
     if (dlv[k] != CELL_BAD) goalset.push_back(dlv[k]);
   }
   TRY(ensure_agents(c, std::max<uint32_t>(n, 1)));
-  if (m > c->tcap || !c->d_used) {
+  if (live.size() > c->tcap || !c->d_live) {
     HIPCHK(hipStreamSynchronize(c->s));
-    size_t a = c->tcap, b = c->tcap, d = c->tcap, e = c->tcap;
-    HIPCHK(dgrow(c->d_pick_xy, a, std::max<uint32_t>(m, 1)));
-    HIPCHK(dgrow(c->d_pick, b, std::max<uint32_t>(m, 1)));
-    HIPCHK(dgrow(c->d_dlv, d, std::max<uint32_t>(m, 1)));
-    HIPCHK(dgrow(c->d_used, e, std::max<uint32_t>(m, 1)));
-    c->tcap = std::min(std::min(a, b), std::min(d, e));
+    size_t a = c->tcap, b = c->tcap, d = c->tcap;
+    HIPCHK(dgrow(c->d_live, a, live.size()));
+    HIPCHK(dgrow(c->d_pick, b, live.size()));
+    HIPCHK(dgrow(c->d_dlv, d, live.size()));
+    c->tcap = std::min(std::min(a, b), d);
     if (!c->d_unused) HIPCHK(hipMalloc(&c->d_unused, 4));
   }
   const size_t stride_t = (size_t)max_t + 1;
@@ -1601,11 +1613,10 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
     HIPCHK(hipMemsetAsync(c->d_st, 0, n, c->s));
     HIPCHK(hipMemsetAsync(c->d_task, 0xFF, n * 4ull, c->s));
   }
+  HIPCHK(hipMemcpyAsync(c->d_live, live.data(), live.size() * 4ull, hipMemcpyHostToDevice, c->s));
   if (m) {
-    HIPCHK(hipMemcpyAsync(c->d_pick_xy, pick_xy.data(), m * 4ull, hipMemcpyHostToDevice, c->s));
     HIPCHK(hipMemcpyAsync(c->d_pick, pick.data(), m * 4ull, hipMemcpyHostToDevice, c->s));
     HIPCHK(hipMemcpyAsync(c->d_dlv, dlv.data(), m * 4ull, hipMemcpyHostToDevice, c->s));
-    HIPCHK(hipMemsetAsync(c->d_used, 0, m, c->s));
   }
   HIPCHK(hipMemcpyAsync(c->d_unused, &m, 4, hipMemcpyHostToDevice, c->s));
   HIPCHK(hipStreamSynchronize(c->s));  // host vectors above go out of scope only at return, but keep it simple
@@ -1838,8 +1849,8 @@ void tsw_destroy(tsw_ctx* c) {
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
   fre(c->d_gt); fre(c->d_dec); fre(c->d_mu); fre(c->d_dups); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
   if (c->h_dups) (void)hipHostFree(c->h_dups);
-  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_pick_xy); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
-  fre(c->d_used); fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
+  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_live); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
+  fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
   fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
@@ -1858,15 +1869,19 @@ const char* tsw_last_error(const tsw_ctx* c) { return c ? c->err.c_str() : g_cre
 
 int tsw_abi_version(void) { return TSW_ABI_VERSION; }
 
+uint64_t tsw_build_id(void) { return (uint64_t)TSW_SRC_HASH; }
+
 int tsw_plan_mapd(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* tasks, uint32_t m,
                   uint32_t max_t, tsw_rec* out, uint32_t* out_T) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   return plan_impl(c, starts, n, tasks, m, max_t, out, nullptr, out_T);
 }
 
 int tsw_plan_mapd_trace(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* tasks, uint32_t m,
                         uint32_t max_t, tsw_rec* out, uint32_t* goal_out, uint32_t* out_T) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   return plan_impl(c, starts, n, tasks, m, max_t, out, goal_out, out_T);
 }
 
@@ -1874,6 +1889,7 @@ int tsw_plan_mapd_resolved(tsw_ctx* c, const tsw_point* starts, uint32_t n, cons
                            uint32_t max_t, tsw_rec* out, uint32_t* goal_out, uint32_t* out_T, tsw_resolve_fn resolve,
                            void* user) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (!resolve) RET(TSW_EINVAL, "null resolver");
   c->resolver = resolve;
   c->resolver_user = user;
@@ -1925,6 +1941,7 @@ int next_hop_codes_impl(tsw_ctx* c, const uint32_t* start, const uint32_t* goal,
 
 int tsw_next_hop_codes(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, uint32_t k, uint8_t* code) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (k == 0) return TSW_OK;
   if (!start || !goal || !code) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -1935,6 +1952,7 @@ int tsw_next_hop_codes(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, 
 
 int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (n == 0) return TSW_OK;
   if (!v || !g) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -2091,6 +2109,7 @@ int tsw_decide(tsw_ctx* c, const uint32_t* my_v, const uint32_t* my_g, uint32_t 
                const uint32_t* nb_v, const uint32_t* nb_g, uint32_t* act, uint32_t* cell, uint32_t* partner,
                uint32_t* npart, uint32_t* part) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   // a failed round may leave queued pairs PENDING: reset them before returning the error
   return reset_pending_after(c, decide_impl(c, my_v, my_g, n, nb_off, nb_v, nb_g, act, cell, partner, npart, part));
 }
@@ -2098,6 +2117,7 @@ int tsw_decide(tsw_ctx* c, const uint32_t* my_v, const uint32_t* my_g, uint32_t 
 int tsw_get_path_next(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, uint32_t k, uint32_t* next,
                       int32_t* len) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (k == 0) return TSW_OK;
   if (!start || !goal || !next || !len) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -2147,6 +2167,7 @@ int tsw_get_path_next(tsw_ctx* c, const uint32_t* start, const uint32_t* goal, u
 
 int tsw_dist_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16_t* out) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (k == 0) return TSW_OK;
   if (!goals || !out) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -2168,6 +2189,7 @@ int tsw_dist_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16_t* out
 
 int tsw_dist_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16_t* dev_out) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (k == 0) return TSW_OK;
   if (!goals || !dev_out) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -2196,6 +2218,7 @@ int tsw_dist_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16
 
 int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, const uint16_t* dev_tables) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (k == 0) return TSW_OK;
   if (!goals || !dev_tables) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -2229,6 +2252,7 @@ int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, cons
 
 int tsw_next_hop_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* out) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (k == 0) return TSW_OK;
   if (!goals || !out) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -2249,6 +2273,7 @@ int tsw_next_hop_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* 
 
 int tsw_next_hop_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint8_t* dev_out, uint16_t* dev_dist) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (k == 0) return TSW_OK;
   if (!goals || !dev_out) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -2289,6 +2314,7 @@ int tsw_next_hop_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, ui
 int tsw_import_next_hops_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, const uint16_t* dev_dist,
                                 const uint8_t* dev_nh) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (k == 0) return TSW_OK;
   if (!goals || !dev_dist || !dev_nh) RET(TSW_EINVAL, "null argument");
   TRY(set_device(c));
@@ -2322,6 +2348,7 @@ int tsw_import_next_hops_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, c
 
 int tsw_clear_tables(tsw_ctx* c) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   TRY(set_device(c));
   HIPCHK(hipStreamSynchronize(c->s));
   std::fill(c->h_goal_tab.begin(), c->h_goal_tab.end(), -1);
@@ -2351,6 +2378,7 @@ int tsw_get_stats(const tsw_ctx* c, tsw_stats* out) {
 
 int tsw_reset_stats(tsw_ctx* c) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   resolve_timing(c);
   const uint64_t tabs = c->st.tables;
   c->st = tsw_stats{};
@@ -2361,6 +2389,7 @@ int tsw_reset_stats(tsw_ctx* c) {
 
 int tsw_set_timing(tsw_ctx* c, int enabled) {
   if (!c) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   resolve_timing(c);
   c->timing = enabled != 0;
   return TSW_OK;
@@ -2368,6 +2397,7 @@ int tsw_set_timing(tsw_ctx* c, int enabled) {
 
 int tsw_probe_round_floors(tsw_ctx* c, uint32_t block, double* out) {
   if (!c || !out) return TSW_EINVAL;
+  NOT_FROM_RESOLVER(c);
   if (block == 0) block = c->st.plan_block ? c->st.plan_block : 1024u;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->s));

@@ -19,6 +19,7 @@ enum : uint32_t {
 };
 enum : uint32_t { PLAN_RUNNING = 0, PLAN_NEED_QUERIES = 1, PLAN_DONE = 2, PLAN_ERROR = 3 };
 enum : uint32_t { MODE_MAPD = 0, MODE_STEP = 1 };
+constexpr uint32_t TASK_TAKEN = 0xFFFFFFFFu;  // PlanArgs::live entry of an assigned task
 
 // Persisted in device memory between launches (exact resume point).
 struct PlanCtl {
@@ -72,10 +73,11 @@ struct PlanArgs {
   uint32_t* mk;   // per agent batch marks of the wave rules rounds (global copy, n + 1 entries)
   uint32_t* occ;  // per cell occupancy
   uint64_t* mu;   // per cell round-tagged lowest undecided targeting agent (global copy)
-  const uint32_t* pick_xy;
+  // K4: per task its pickup point (x | y << 16, coordinates clamped to 0xFFFE) while unused, TASK_TAKEN
+  // once assigned; padded with TASK_TAKEN to a multiple of 4 entries (the scan reads 16-B vectors)
+  uint32_t* live;
   const uint32_t* pick;
   const uint32_t* dlv;
-  uint8_t* used;
   const int32_t* goal_tab;
   uint8_t* nh;
   uint64_t nstride;

@@ -88,8 +88,7 @@ struct Arrays {
   uint32_t* F2;
   uint32_t* OCC;   // per cell: lowest agent | OCC_FLAG, or OCC_NONE
   uint64_t* MU;    // per cell: (round << 32) | ~(lowest undecided agent targeting it), movement rounds
-  const uint32_t* PXY;
-  uint8_t* USED;
+  uint32_t* LIVE;  // K4: pickup point of each unused task, TASK_TAKEN once assigned (PlanArgs::live)
   unsigned long long t0;  // wall clock at the launch (coop: "no worker has started" is measured from here)
 };
 
@@ -762,7 +761,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     return;
   }
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[6], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort, s_hops;
+  __shared__ uint32_t s_q[6], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort, s_hops,
+      s_badat;
   __shared__ uint32_t s_ap[128];  // rules: members of a rule-4 cycle rotated by the wave (<= 64), links
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
@@ -848,16 +848,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     S.MU = P.mu;
   }
   if (P.tasks_lds) {
-    uint32_t* pxy = reinterpret_cast<uint32_t*>(carve((size_t)P.m * 4));
-    S.USED = carve(P.m);
-    S.PXY = pxy;
-    for (uint32_t k = tid; k < P.m; k += bd) {
-      pxy[k] = P.pick_xy[k];
-      S.USED[k] = P.used[k];
-    }
+    S.LIVE = reinterpret_cast<uint32_t*>(carve((size_t)((P.m + 3u) & ~3u) * 4));
+    for (uint32_t k = tid; k < ((P.m + 3u) & ~3u); k += bd) S.LIVE[k] = P.live[k];
   } else {
-    S.PXY = P.pick_xy;
-    S.USED = P.used;
+    S.LIVE = P.live;
   }
   for (uint32_t k = tid; k <= n; k += bd) S.MK[k] = 0xFFFFFFFFu;
   for (uint32_t k = tid; k < n; k += bd) {
@@ -948,19 +942,51 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     }
     if (sec == SEC_ASSIGN) {
       // ---- K4: state machine + task assignment (tswap.rs:106-139) -------------
+      // The reference walks agents in index order: an agent at its goal advances its state (ToPickup ->
+      // ToDelivery with g := delivery, :107-118; ToDelivery -> Idle, :119-121), then an Idle agent takes
+      // the nearest unused pickup (:123-138). Transitions touch only their own agent, so they run in
+      // parallel; the assignments depend on each other (a task taken by an earlier agent is gone) and
+      // run one after another in index order, each a block-wide argmin over the LIVE array. The first
+      // agent whose delivery cell is bad (pos2id panics, :112) ends the step there: assignments of
+      // agents below it still happen (and may panic first, :136), none above it.
       if (tid == 0) s_nassign = s_npick = s_bad = 0;
       __syncthreads();
+      const uint32_t m4 = (P.m + 3u) & ~3u;
       for (uint32_t base = 0; base < n && !s_bad; base += bd) {
         const uint32_t i = base + tid;
-        bool needy = false;
+        bool idle = false;
+        if (tid == 0) s_badat = NO_AGENT;  // lowest agent of this chunk with a bad delivery cell
+        __syncthreads();
         if (i < n) {
-          const uint8_t st = P.st[i];
-          needy = (S.V[i] == S.G[i] && st != ST_IDLE) || (st == ST_IDLE && s_ctl.unused > 0u);
+          uint8_t st = P.st[i];
+          if (S.V[i] == S.G[i] && st != ST_IDLE) {
+            if (st == ST_TO_PICKUP) {
+              st = ST_TO_DELIVERY;
+              atomicAdd(&s_npick, 1u);
+              if (P.dbg) S.DEC[i] = 0x41;  // diagnostics tag (MOVE re-initialises DEC)
+              const int32_t tk = P.task[i];
+              if (tk >= 0) {
+                const uint32_t ng = P.dlv[tk];
+                if (ng == CELL_BAD) {  // pos2id[&task.delivery] panics (tswap.rs:112)
+                  atomicMin(&s_badat, i);
+                } else {
+                  S.G[i] = ng;
+                  S.GT[i] = P.goal_tab[ng];
+                  S.NHC[i] = NHC_DIRTY;
+                }
+              }
+            } else {  // ST_TO_DELIVERY
+              st = ST_IDLE;
+              P.task[i] = -1;
+            }
+            P.st[i] = st;
+          }
+          idle = st == ST_IDLE;
         }
-        const uint64_t bal = __ballot(needy);
+        const uint64_t bal = __ballot(idle);
         if (lane == 0) s_wcount[wid] = (uint32_t)__popcll(bal);
         __syncthreads();
-        if (needy) {
+        if (idle) {
           uint32_t off = 0;
           for (uint32_t w = 0; w < wid; ++w) off += s_wcount[w];
           off += (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
@@ -972,79 +998,80 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
           s_cnt = c;
         }
         __syncthreads();
-        const uint32_t cnt = s_cnt;
+        const uint32_t cnt = s_cnt, bad_at = s_badat;
         for (uint32_t kk = 0; kk < cnt && !s_bad; ++kk) {
           const uint32_t ai = list[kk];
-          if (tid == 0) {
-            const uint32_t v = S.V[ai];
-            uint8_t st = P.st[ai];
-            if (v == S.G[ai]) {
-              if (st == ST_TO_PICKUP) {
-                st = ST_TO_DELIVERY;
-                ++s_npick;
-                if (P.dbg) S.DEC[ai] = 0x41;  // diagnostics tag (MOVE re-initialises DEC)
-                const int32_t tk = P.task[ai];
-                if (tk >= 0) {
-                  const uint32_t ng = P.dlv[tk];
-                  if (ng == CELL_BAD) {  // pos2id[&task.delivery] panics (tswap.rs:112)
-                    atomicOr(&P.ctl->err, ERR_BAD_DELIVERY);
-                    s_bad = 1;
-                  } else {
-                    S.G[ai] = ng;
-                    S.GT[ai] = P.goal_tab[ng];
-                    S.NHC[ai] = NHC_DIRTY;
-                  }
-                }
-              } else if (st == ST_TO_DELIVERY) {
-                st = ST_IDLE;
-                P.task[ai] = -1;
-              }
-              P.st[ai] = st;
+          if (ai > bad_at || s_ctl.unused == 0u) break;  // block-uniform: LDS values read after a barrier
+          const uint32_t v = S.V[ai];
+          const uint32_t px = v % W, py = v / W;
+          // first minimum of (Manhattan(pos, pickup), task index) over unused tasks (min_by_key, :125-130)
+          uint64_t best = ~0ull;
+          if (P.tasks_lds) {
+            for (uint32_t t = tid; t < P.m; t += bd) {
+              const uint32_t xy = S.LIVE[t];
+              const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
+              const uint32_t d = (px > tx ? px - tx : tx - px) + (py > ty ? py - ty : ty - py);
+              const uint64_t key = xy == TASK_TAKEN ? ~0ull : (((uint64_t)d << 32) | t);
+              best = key < best ? key : best;
             }
-            s_doit = (st == ST_IDLE && s_ctl.unused > 0u) ? 1u : 0u;
-            s_px = v % W;
-            s_py = v / W;
+          } else {
+            // 16-B vectors, lane-interleaved (one coalesced 1 KB read per wave per vector), up to eight in
+            // flight per lane: C3's 32,000 tasks are one pass of eight loads per lane
+            const uint4* L4 = reinterpret_cast<const uint4*>(S.LIVE);
+            const uint32_t q4 = m4 >> 2;
+            constexpr uint32_t VL = 8u;
+            for (uint32_t j0 = tid; j0 < q4; j0 += VL * bd) {
+              uint4 a[VL];
+#pragma unroll
+              for (uint32_t u = 0; u < VL; ++u)
+                a[u] = j0 + u * bd < q4 ? L4[j0 + u * bd] : make_uint4(TASK_TAKEN, TASK_TAKEN, TASK_TAKEN, TASK_TAKEN);
+#pragma unroll
+              for (uint32_t u = 0; u < VL; ++u) {
+                const uint32_t xs[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+#pragma unroll
+                for (uint32_t e = 0; e < 4u; ++e) {
+                  const uint32_t xy = xs[e];
+                  const uint32_t t = (j0 + u * bd) * 4u + e;
+                  const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
+                  const uint32_t d = (px > tx ? px - tx : tx - px) + (py > ty ? py - ty : ty - py);
+                  const uint64_t key = xy == TASK_TAKEN ? ~0ull : (((uint64_t)d << 32) | t);
+                  best = key < best ? key : best;
+                }
+              }
+            }
+          }
+          best = wave_min_u64(best);
+          if (lane == 0) s_red[wid] = best;
+          __syncthreads();
+          if (tid == 0) {
+            uint64_t b = ~0ull;
+            for (uint32_t w = 0; w < nwaves; ++w) b = s_red[w] < b ? s_red[w] : b;
+            if (b != ~0ull) {  // first minimum (min_by_key, tswap.rs:130)
+              const uint32_t t = (uint32_t)(b & 0xFFFFFFFFu);
+              S.LIVE[t] = TASK_TAKEN;
+              if (P.tasks_lds) P.live[t] = TASK_TAKEN;
+              s_ctl.unused -= 1u;
+              P.task[ai] = (int32_t)t;
+              P.st[ai] = ST_TO_PICKUP;
+              ++s_nassign;
+              if (P.dbg) S.DEC[ai] = 0x40;
+              const uint32_t ng = P.pick[t];
+              if (ng == CELL_BAD) {  // pos2id[&task.pickup] panics (tswap.rs:136)
+                atomicOr(&P.ctl->err, ERR_BAD_PICKUP);
+                s_bad = 1;
+              } else {
+                S.G[ai] = ng;
+                S.GT[ai] = P.goal_tab[ng];
+                S.NHC[ai] = NHC_DIRTY;
+              }
+            }
           }
           __syncthreads();
-          if (s_bad) break;  // block-uniform: the reference panicked on this agent
-          if (s_doit) {
-            const uint32_t px = s_px, py = s_py;
-            uint64_t best = ~0ull;
-            for (uint32_t t = tid; t < P.m; t += bd) {
-              if (!S.USED[t]) {
-                const uint32_t xy = S.PXY[t];
-                const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
-                const uint32_t d = (px > tx ? px - tx : tx - px) + (py > ty ? py - ty : ty - py);
-                const uint64_t key = ((uint64_t)d << 32) | t;
-                best = key < best ? key : best;
-              }
-            }
-            best = wave_min_u64(best);
-            if (lane == 0) s_red[wid] = best;
-            __syncthreads();
-            if (tid == 0) {
-              uint64_t b = ~0ull;
-              for (uint32_t w = 0; w < nwaves; ++w) b = s_red[w] < b ? s_red[w] : b;
-              if (b != ~0ull) {  // first minimum (min_by_key, tswap.rs:130)
-                const uint32_t t = (uint32_t)(b & 0xFFFFFFFFu);
-                S.USED[t] = 1;
-                if (P.tasks_lds) P.used[t] = 1;
-                s_ctl.unused -= 1u;
-                P.task[ai] = (int32_t)t;
-                P.st[ai] = ST_TO_PICKUP;
-                ++s_nassign;
-                if (P.dbg) S.DEC[ai] = 0x40;
-                const uint32_t ng = P.pick[t];
-                if (ng == CELL_BAD) {  // pos2id[&task.pickup] panics (tswap.rs:136)
-                  atomicOr(&P.ctl->err, ERR_BAD_PICKUP);
-                  s_bad = 1;
-                } else {
-                  S.G[ai] = ng;
-                  S.GT[ai] = P.goal_tab[ng];
-                  S.NHC[ai] = NHC_DIRTY;
-                }
-              }
-            }
+        }
+        if (bad_at != NO_AGENT && !s_bad) {  // block-uniform
+          if (tid == 0) {
+            atomicOr(&P.ctl->err, ERR_BAD_DELIVERY);
+            s_bad = 1;
           }
           __syncthreads();
         }
@@ -2155,7 +2182,7 @@ size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool 
     if (flinks) b += 2 * r16((size_t)(n + 1) * 4);
   }
   if (occ) b += r16((size_t)ncell * 4) + (mu ? r16((size_t)ncell * 8) : 0u);
-  if (tasks) b += r16((size_t)m * 4) + r16(m);
+  if (tasks) b += r16((size_t)((m + 3u) & ~3u) * 4);
   return b;
 }
 

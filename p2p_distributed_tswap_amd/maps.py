@@ -258,20 +258,81 @@ def make_window_instance(rows, n_agents: int, n_tasks: int, seed: int, x0: int, 
     return starts, tasks
 
 
-def c5_instance(n_agents: int = 10000, n_tasks: int = 10000, seed: int = 0x1024):
-    """C5: the 1024x1024 sortation floor, agents and task cells packed into the central
-    160x160 window (~24k free cells, 10k agents = ~42% occupancy): dense traffic, rule-3 swaps and
-    rule-4 rotation cycles every step. Returns (rows, starts, tasks)."""
+def make_wf_instance(rows, n_agents: int, n_tasks: int, seed: int, window=None):
+    """Well-formed MAPD instance (round 5): n distinct start (parking) cells, and
+    n_tasks (pickup != delivery) pairs whose endpoints are drawn from the OTHER free cells of the
+    largest component (optionally of the window (x0, y0, w, h)), so no task endpoint is a start cell.
+
+    Why it matters for the reference loop: an Idle agent keeps g = v (tswap.rs:92-101, :119-121);
+    an agent whose goal is the cell such an agent rests on gets a rule-3 swap of two EQUAL goals
+    (tswap.rs:198-202), a no-op, and the plan spins to `timestep > 2000` (:167) with nothing moving.
+    With endpoints disjoint from the parking cells and a task stream that outlasts the horizon (an
+    agent that delivers takes its next task in the same ASSIGN pass, :119-139), no agent parks and
+    every timestep moves agents. Returns (starts (n,2) uint32, tasks (m,4) uint32 [px,py,dx,dy])."""
+    cells = largest_component(rows)
+    if window is not None:
+        x0, y0, w, h = window
+        cells = [c for c in cells if x0 <= c[0] < x0 + w and y0 <= c[1] < y0 + h]
+    r = SplitMix64(seed ^ 0xC3C3C3C3)
+    pool = list(cells)
+    r.shuffle(pool)
+    if n_agents + 2 > len(pool):
+        raise ValueError("more agents than free cells (two task endpoints must remain)")
+    starts = np.array(pool[:n_agents], dtype=np.uint32).reshape(-1, 2)
+    ep = pool[n_agents:]
+    ne = len(ep)
+    tasks = np.zeros((n_tasks, 4), dtype=np.uint32)
+    for k in range(n_tasks):
+        a = r.below(ne)
+        b = r.below(ne - 1)
+        if b >= a:
+            b += 1
+        tasks[k] = (*ep[a], *ep[b])
+    return starts, tasks
+
+
+C5_WINDOW = (432, 432, 160, 160)
+
+
+def c5_instance(n_agents: int = 10000, n_tasks: int = 24000, seed: int = 0x1024):
+    """C5 (BASELINE configs[4]): the 1024x1024 sortation floor, agents and task cells packed
+    into the central 160x160 window (~24k free cells, 10k agents = ~42% occupancy): dense traffic,
+    rule-3 swaps and rule-4 rotation cycles every step. Well-formed (make_wf_instance) with a
+    24,000-task stream: ~10k deliveries in 2,001 steps, so the stream outlasts the horizon and every
+    timestep moves agents. Returns (rows, starts, tasks)."""
     rows = sortation_map(1024, 1024)
-    starts, tasks = make_window_instance(rows, n_agents, n_tasks, seed, 432, 432, 160, 160)
+    starts, tasks = make_wf_instance(rows, n_agents, n_tasks, seed, C5_WINDOW)
     return rows, starts, tasks
 
 
-def wh10k_instance(n_agents: int = 10000, n_tasks: int = 30000, seed: int = 0x510220):
+def wh10k_instance(n_agents: int = 10000, n_tasks: int = 40000, seed: int = 0x510220):
     """The north_star's "10k-agent warehouse": the warehouse generator at 510x220 (shelf blocks,
-    1-wide aisles), 10,000 agents, 30,000-task MAPD stream. Returns (rows, starts, tasks)."""
+    1-wide aisles), 10,000 agents, a well-formed 40,000-task MAPD stream (outlasts 2,001 steps).
+    Returns (rows, starts, tasks)."""
+    rows = warehouse_map(510, 220, seed)
+    starts, tasks = make_wf_instance(rows, n_agents, n_tasks, seed)
+    return rows, starts, tasks
+
+
+# ---- round-1..4 instances (kept as extra parity tests) -------------------------------------
+# Task endpoints drawn from all free cells (start cells included) and streams shorter than the
+# horizon: the plans freeze once the stream is spent (C3 from t = 446, C5 from t = 152, wh10k from
+# t = 1,282 — VERDICT r4 missing #1). Their full-horizon digests stay committed.
+def c5_legacy_instance(n_agents: int = 10000, n_tasks: int = 10000, seed: int = 0x1024):
+    rows = sortation_map(1024, 1024)
+    starts, tasks = make_window_instance(rows, n_agents, n_tasks, seed, *C5_WINDOW)
+    return rows, starts, tasks
+
+
+def wh10k_legacy_instance(n_agents: int = 10000, n_tasks: int = 30000, seed: int = 0x510220):
     rows = warehouse_map(510, 220, seed)
     starts, tasks = make_instance(rows, n_agents, n_tasks, seed)
+    return rows, starts, tasks
+
+
+def c3_legacy_instance():
+    rows = warehouse_map(170, 84, 0x170084)
+    starts, tasks = make_instance(rows, 1000, 3000, 0x170084)
     return rows, starts, tasks
 
 
@@ -279,21 +340,37 @@ CONFIGS = {
     # name: (map factory, n_agents, n_tasks, instance seed)  — BASELINE.json configs
     "c1_bundled_10": (bundled_map, 10, 30, 1),
     "c2_random_32_32_20": (lambda: random_map(32, 32, 0.20, 0x3232), 200, 600, 0x3232),
-    "c3_warehouse_170x84": (lambda: warehouse_map(170, 84, 0x170084), 1000, 3000, 0x170084),
+    # well-formed, 32,000-task stream: ~24k deliveries in 2,001 steps, every timestep moves agents
+    "c3_warehouse_170x84": (lambda: warehouse_map(170, 84, 0x170084), 1000, 32000, 0x170084),
     # K1-only config: 10,000 distinct goal cells (BFS tables), goal-sharded over 2/4/8 GPUs
     "c4_den520d_10k_goals": (lambda: cave_map(256, 257, 0x520D), 0, 0, 0x520D),
     # dense MAPD on the sortation floor: instance from c5_instance() (window-packed, not make_instance)
-    "c5_sortation_1024_10k": (lambda: sortation_map(1024, 1024), 10000, 10000, 0x1024),
+    "c5_sortation_1024_10k": (lambda: sortation_map(1024, 1024), 10000, 24000, 0x1024),
 }
+# configs whose instance is well-formed (make_wf_instance)
+WELL_FORMED = {"c3_warehouse_170x84", "c5_sortation_1024_10k"}
 # distinct K1 goals of the table-build configs
 CONFIG_GOALS = {"c4_den520d_10k_goals": 10000, "c5_sortation_1024_10k": 10000}
 
 
-def config_instance(name: str):
-    """(rows, starts, tasks) of a MAPD config of CONFIGS."""
-    if name == "c5_sortation_1024_10k":
-        return c5_instance()
+def config_instance(name: str, seed_offset: int = 0):
+    """(rows, starts, tasks) of a MAPD config of CONFIGS; seed_offset draws another instance of the same
+    shape on the same map (bench.py's replicas: seed + rank)."""
     fac, n, m, seed = CONFIGS[name]
+    if name == "c5_sortation_1024_10k":
+        return c5_instance(n, m, seed + seed_offset)
     rows = fac()
-    starts, tasks = make_instance(rows, n, m, seed)
+    if name in WELL_FORMED:
+        starts, tasks = make_wf_instance(rows, n, m, seed + seed_offset)
+    else:
+        starts, tasks = make_instance(rows, n, m, seed + seed_offset)
     return rows, starts, tasks
+
+
+def moving_timesteps(rec: np.ndarray) -> int:
+    """Timesteps t >= 1 of a plan (records (n, T), x | y<<16 | state<<32) in which at least one agent's
+    position differs from t - 1 (VERDICT r4 #1: report how much of a horizon actually plans)."""
+    pos = np.asarray(rec, dtype=np.uint64) & np.uint64(0xFFFFFFFF)
+    if pos.shape[1] < 2:
+        return 0
+    return int(np.count_nonzero((pos[:, 1:] != pos[:, :-1]).any(axis=0)))

@@ -35,7 +35,7 @@ pub const TSW_ENODEV: c_int = -19;
 
 /// ABI revision of include/tswap.h this crate mirrors; `Planner::new` refuses a library built
 /// against another one.
-pub const TSW_ABI_VERSION: c_int = 4;
+pub const TSW_ABI_VERSION: c_int = 5;
 
 pub const TSW_PICKING: u8 = 0;
 pub const TSW_CARRYING: u8 = 1;
@@ -139,6 +139,7 @@ extern "C" {
                                   resolve: TswResolveFn, user: *mut c_void) -> c_int;
     pub fn tsw_next_hop_codes(ctx: *mut TswCtx, start: *const u32, goal: *const u32, k: u32, code: *mut u8) -> c_int;
     pub fn tsw_abi_version() -> c_int;
+    pub fn tsw_build_id() -> u64;
     pub fn tsw_plan_mapd(ctx: *mut TswCtx, starts: *const TswPoint, n: u32, tasks: *const TswTask, m: u32,
                          max_t: u32, out: *mut TswRec, out_t: *mut u32) -> c_int;
     pub fn tsw_plan_mapd_trace(ctx: *mut TswCtx, starts: *const TswPoint, n: u32, tasks: *const TswTask, m: u32,

@@ -10,7 +10,7 @@
 # Then: python scripts/summarize_profile.py $OUT profiles/<tag>
 # Each GPU step has its own time limit; steps are chained with && so a failure stops the run.
 set -o pipefail
-TAG=${1:-r4}
+TAG=${1:-r5}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp

@@ -8,9 +8,10 @@ baseline) plans a bounded PREFIX of timesteps, is timed, and its prefix is compa
 with the GPU's. CPU whole-plan time is extrapolated from the prefix rate (labelled as such).
 
 usage: python scripts/scale_bench.py [instance ...] [--cpu-steps N]
-instances: c3 (warehouse 170x84, 1,000 agents, 3,000 tasks — BASELINE configs[2]),
-           wh10k (warehouse 510x220, 10,000 agents, 30,000 tasks — the north_star instance),
-           c5 (1024x1024 sortation floor, 10,000 agents packed in a 160x160 window — configs[4])
+instances: c3 (warehouse 170x84, 1,000 agents, well-formed 32,000-task stream — BASELINE configs[2]),
+           wh10k (warehouse 510x220, 10,000 agents, well-formed 40,000 tasks — the north_star instance),
+           c5 (1024x1024 sortation floor, 10,000 agents packed in a 160x160 window, 24,000 tasks — configs[4]),
+           c3_legacy / wh10k_legacy / c5_legacy: the round-1..4 instances (plans freeze before the cap)
 """
 import argparse
 import json
@@ -24,15 +25,14 @@ import numpy as np  # noqa: E402
 
 from p2p_distributed_tswap_amd import Planner, maps  # noqa: E402
 
-def _wh10k():
-    return maps.wh10k_instance()
-
-
 # name: (instance factory -> (rows, starts, tasks), CPU prefix timesteps)
 INSTANCES = {
     "c3": (lambda: maps.config_instance("c3_warehouse_170x84"), 20),
-    "wh10k": (_wh10k, 3),
+    "wh10k": (maps.wh10k_instance, 3),
     "c5": (maps.c5_instance, 2),
+    "c3_legacy": (maps.c3_legacy_instance, 20),
+    "wh10k_legacy": (maps.wh10k_legacy_instance, 3),
+    "c5_legacy": (maps.c5_legacy_instance, 2),
 }
 
 
@@ -107,6 +107,7 @@ def main():
         cpu_rate = n * ct / cpu_s
         out = {
             "instance": name, "grid": f"{w}x{h}", "agents": n, "tasks": m, "timesteps": int(T),
+            "timesteps_moving": maps.moving_timesteps(rec),
             "gpu_end_to_end_s": round(gpu_s, 3), "gpu_agent_steps_per_s": round(n * T / gpu_s, 1),
             "cpu_prefix_timesteps": int(ct), "cpu_prefix_s": round(cpu_s, 3),
             "cpu_agent_steps_per_s": round(cpu_rate, 1),

@@ -66,13 +66,16 @@ def bench_line(path: str):
 
 def main(src: str, dst: str):
     os.makedirs(dst, exist_ok=True)
-    out = {"source": src, "correction": "read = 2*FETCH_SIZE KB, write = WRITE_SIZE KB (gfx950)", "workloads": {}}
+    out = {"source": src, "correction": "read = 2*FETCH_SIZE KB, write = WRITE_SIZE KB (gfx950)", "workloads": {},
+           "build_id": None}
+    builds = set()
     for wl, key in WORKLOADS.items():
         stats = os.path.join(src, f"{wl}_trace", "run_kernel_stats.csv")
         line = bench_line(os.path.join(src, f"{wl}_trace.json"))
         if not os.path.exists(stats) or line is None:
             continue
         shutil.copy(stats, os.path.join(dst, f"{wl}_kernel_stats.csv"))
+        builds.add(line.get("build_id"))
         cls = collections.defaultdict(lambda: {"device_ns": 0.0, "dispatches": 0, "kernels": {}})
         for r in csv.DictReader(open(stats)):
             c = kclass(r["Name"])
@@ -135,6 +138,12 @@ def main(src: str, dst: str):
                     e["queries"] = int(ks.get("astar_queries", 0))
             res[c] = e
         out["workloads"][key] = res
+    # provenance: the library build every profiled run loaded; bench.py pairs this file
+    # only with that build. Runs of different builds in one directory: no build_id, nothing is paired.
+    if len(builds) == 1:
+        out["build_id"] = builds.pop()
+    else:
+        out["build_ids_seen"] = sorted(str(b) for b in builds)
     bj = os.path.join(src, "bench.json")
     if os.path.exists(bj):
         shutil.copy(bj, os.path.join(dst, "bench.json"))

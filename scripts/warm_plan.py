@@ -13,7 +13,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from p2p_distributed_tswap_amd import Planner, maps  # noqa: E402
+from p2p_distributed_tswap_amd import Planner, build_id, maps  # noqa: E402
 
 
 def main():
@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     rows, starts, tasks = maps.config_instance(a.config)
-    out = {"config": a.config, "cold_ms": [], "warm_ms": [], "warm_waits": [], "cold_waits": [],
+    out = {"config": a.config, "build_id": build_id(), "cold_ms": [], "warm_ms": [], "warm_waits": [], "cold_waits": [],
            "cold_queries": [], "warm_queries": []}
     with Planner(rows) as p:
         p.plan_mapd_arrays(starts, tasks, 50)
@@ -41,6 +41,7 @@ def main():
             out["warm_waits"].append(p.stats()["coop_waits"])
             out["warm_queries"].append(p.stats()["astar_queries"])
             assert (rec == ref).all()
+            out["agent_steps"] = int(rec.shape[0] * rec.shape[1])
     print(json.dumps(out), flush=True)
 
 

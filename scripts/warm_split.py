@@ -46,9 +46,10 @@ def main():
 
     cold, warm = bytes_of(1), bytes_of(2)
     q = wj["cold_queries"][0]
-    agent_steps = 1000 * 2001  # C3: 1,000 agents x 2,001 recorded timesteps
+    agent_steps = wj.get("agent_steps", 1000 * 2001)  # agents x recorded timesteps of the plan
     out = {
         "config": wj["config"],
+        "build_id": wj.get("build_id"),
         "method": "PMC FETCH_SIZE / WRITE_SIZE of the cold and the warm coop plan dispatch (scripts/warm_plan.py)",
         "cold_dispatch_bytes": round(cold),
         "warm_dispatch_bytes": round(warm),

@@ -1,13 +1,15 @@
 """GPU parity on the BASELINE configs at their real sizes (VERDICT r1 "close the untested configs").
 
-* C3 (configs[2]): warehouse 170x84, 1,000 agents, 3,000 tasks, full horizon (cap 2000) — every
-  timestep's records and goals against the oracle's per-timestep digests (tests/golden/digests.json,
-  made by tests/golden/make_digests.py; the oracle needs ~75 s for this plan, the GPU ~1 s).
+* C3 (configs[2]): warehouse 170x84, 1,000 agents, well-formed 32,000-task stream, full horizon (cap
+  2000) — every timestep's records and goals against the oracle's per-timestep digests
+  (tests/golden/digests_c3_busy.json, made by tests/golden/make_digests.py). Every one of its 2,001
+  timesteps moves agents (round 5; the round-1..4 instance, which froze from t = 446, stays as
+  `c3_full`).
 * C5 (configs[4]): 1024x1024 sortation floor, 10,000 agents packed in a 160x160 window (dense
   traffic, rule-3 swaps and rule-4 rotations every step):
     - K1 tables of a seeded goal sample vs the oracle BFS,
     - next hops (get_path(...)[1] and len) on random pairs vs the oracle A*,
-    - a 6-timestep MAPD prefix vs the oracle digests.
+    - a 6-timestep MAPD prefix and the full horizon vs the oracle digests.
 Reference: tswap.rs:39-172 (tswap_mapd), :174-286 (tswap_step), :288-390 (get_path)."""
 import json
 import os
@@ -41,11 +43,25 @@ def _check_digests(name, rec, goals):
     assert not bad, f"{name}: first divergent timestep {bad[0]} ({len(bad)} of {ref['T']})"
 
 
-def test_c3_full_horizon_matches_oracle():
-    rows, starts, tasks = maps.config_instance("c3_warehouse_170x84")
+def _plan_against_digests(name):
+    import sys
+
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_digests import instances
+
+    ref, _ = _digests(name)
+    fac, max_t, _ = instances()[name]
+    assert max_t == ref["max_t"]
+    rows, starts, tasks = fac()
     with Planner(rows) as p:
-        rec, goals = p.plan_mapd_arrays(starts, tasks, 2000, trace_goals=True)
-    _check_digests("c3_full", rec, goals)
+        rec, goals = p.plan_mapd_arrays(starts, tasks, max_t, trace_goals=True)
+    _check_digests(name, rec, goals)
+
+
+@pytest.mark.parametrize("name", ["c3_busy_full", "c3_full"])
+def test_c3_full_horizon_matches_oracle(name):
+    """C3 over the full horizon: the busy well-formed instance (the bench's) and the legacy one."""
+    _plan_against_digests(name)
 
 
 @pytest.fixture(scope="module")
@@ -86,28 +102,23 @@ def test_c5_mapd_prefix(c5):
     rows, starts, tasks, og = c5
     with Planner(rows) as p:
         rec, goals = p.plan_mapd_arrays(starts, tasks, 6, trace_goals=True)
-    _check_digests("c5_prefix", rec, goals)
+    ref, step_digests = _digests("c5_busy_p50")  # a 6-step plan = the first 7 digests of the prefix
+    assert step_digests(rec, goals) == ref["digests"][:7]
 
 
-@pytest.mark.parametrize("name", ["wh10k_p300", "wh10k_full"])
+@pytest.mark.parametrize("name", ["wh10k_busy_p100", "wh10k_busy_full", "wh10k_p300", "wh10k_full"])
 def test_wh10k_long_horizon_matches_oracle(name):
-    """the north_star's 10k-agent warehouse (510x220, 10,000 agents, 30,000 tasks) over
-    300 timesteps and over the full horizon (2,001), every timestep's records and goals against the
-    oracle's digests — the incremental relabels, batched rule-3 firings and the coop PENDING
-    protocol reach their long-tail states only late in a plan."""
-    ref, _ = _digests(name)
-    rows, starts, tasks = maps.wh10k_instance()
-    with Planner(rows) as p:
-        rec, goals = p.plan_mapd_arrays(starts, tasks, ref["max_t"], trace_goals=True)
-    _check_digests(name, rec, goals)
+    """the north_star's 10k-agent warehouse (510x220, 10,000 agents) over the
+    full horizon (2,001 timesteps), every timestep's records and goals against the oracle's digests —
+    the busy well-formed 40,000-task instance (every timestep moves agents, so the incremental
+    relabels, batched rule-3 firings and the coop PENDING protocol run all the way), its plain-oracle
+    100-step prefix, and the legacy 30,000-task instance (frozen from t = 1,282)."""
+    _plan_against_digests(name)
 
 
-@pytest.mark.parametrize("name", ["c5_p300", "c5_full"])
+@pytest.mark.parametrize("name", ["c5_busy_p50", "c5_busy_full", "c5_p300", "c5_full"])
 def test_c5_long_horizon_matches_oracle(name):
-    """C5 (1024x1024 sortation floor, 10,000 agents in dense rotation traffic) over 300
-    timesteps and over the full horizon, against the oracle's per-timestep digests."""
-    ref, _ = _digests(name)
-    rows, starts, tasks = maps.c5_instance()
-    with Planner(rows) as p:
-        rec, goals = p.plan_mapd_arrays(starts, tasks, ref["max_t"], trace_goals=True)
-    _check_digests(name, rec, goals)
+    """C5 (1024x1024 sortation floor, 10,000 agents in dense rotation traffic)
+    over the full horizon against the oracle's per-timestep digests: the busy well-formed 24,000-task
+    instance, its plain-oracle prefix, and the legacy instance (frozen from t = 152)."""
+    _plan_against_digests(name)
