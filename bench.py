@@ -32,10 +32,12 @@ Extra objects on the line:
                 prefix of the same instance on one pinned host core, rank 0 only; its prefix is
                 also compared bit-exactly with the GPU plan, and the GPU plans the SAME prefix
                 (same max_t, from an empty table store) for a like-for-like rate.
-  sharded_plan  N > 1 only: C5 (configs[4]) planned once on rank 0 with its K3 sharded per step by
-                goal owner across all ranks (tsw_plan_mapd_resolved + sharding.ShardedK3, RCCL),
-                timed against rank 0's replica plan of C5 alone, bit-exact against it. The goal-
-                sharded K1 + all-gather is in the `bfs` object (den520d).
+  sharded_plan  N > 1 with --sharded-k3 only: C5 (configs[4]) planned once on rank 0 with its K3
+                sharded per step by goal owner across all ranks (tsw_plan_mapd_resolved +
+                sharding.ShardedK3, RCCL), timed against rank 0's replica plan of C5 alone. Off by
+                default: a plan's K3 time is the latency of single queries, which more GPUs do not
+                shorten (Multi-GPU, has the model). The N > 1 data path is the goal-sharded
+                K1 + RCCL all-gather in the `bfs` object (den520d, configs[3]).
 """
 from __future__ import annotations
 
@@ -63,7 +65,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-bfs", action="store_true", help="skip the K1 BFS measurement")
     ap.add_argument("--no-plan", action="store_true", help="skip the planning leg (profiling K1 alone)")
-    ap.add_argument("--no-sharded", action="store_true", help="N > 1: skip the sharded-K3 C5 leg")
+    ap.add_argument("--sharded-k3", action="store_true",
+                    help="N > 1: also run the sharded-K3 C5 leg (per-step query batches by goal owner); a measured "
+                         "null result, off by default (DESIGN.md, Multi-GPU)")
     ap.add_argument("--diag", action="store_true", help="diagnostic library (TSW_* A/B knobs; not the product)")
     ap.add_argument("--exit-mode", action="store_true",
                     help="TSW_F_EXIT_MODE: no K3 workers in the plan dispatch (K3 as host-launched passes) — "
@@ -462,7 +466,7 @@ def main():
         latency = latency_roofline(st, us_wave, us_pass)
 
     sharded = None
-    if world > 1 and not args.no_plan and not args.no_sharded:
+    if world > 1 and not args.no_plan and args.sharded_k3:
         sharded = sharded_plan_leg(args, rank, world, dev, dist, barrier, allmax)
 
     # K1 BFS alone, den520d-like, 10k distinct goals (configs[3]); rank-local shard of the goals

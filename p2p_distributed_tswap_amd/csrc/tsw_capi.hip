@@ -512,19 +512,28 @@ void bfs_lpt_order(tsw_ctx* c, std::vector<uint32_t>& goals, std::vector<uint32_
   slots.swap(s2);
 }
 
-int ensure_astar_scratch(tsw_ctx* c) {
-  if (c->d_heaps) return TSW_OK;
+// A* scratch slots (global g-scores + overflow heap, one per K3 wave), allocated for the waves that run:
+// `need` slots (0: what a host-launched K3 pass uses, astar_wave_slots), grown on demand, at least 64 and
+// at most 4,096 / a 32 GB cap. A coop dispatch asks for exactly its worker waves (C5's
+// 2,295 workers x 4.5 MB = 10.3 GB instead of a fixed 20 GB budget).
+int ensure_astar_scratch(tsw_ctx* c, uint32_t need = 0) {
   const uint64_t ncell = c->G.ncell;
-  c->hcap = (uint32_t)std::min<uint64_t>(4ull * ncell + 8ull, 1ull << 16);
-  const uint64_t per_slot = (uint64_t)c->hcap * 8ull + ncell * 4ull;
-  // one slot (global g-scores + overflow heap) per K3 wave: a coop dispatch has at most 16 worker waves
-  // on each of the other CUs, so 4,096 slots cover every worker. A 4 GB budget capped C5's 2^20-cell
-  // slots (4.5 MB each) at 910 workers whatever the LDS allowed; 20 GB of the 288 GB lets C5 run as
-  // many workers as its LDS carve fits (round 4)
-  const uint64_t budget = 20ull << 30;
-  uint64_t ns = budget / per_slot;
-  ns = std::max<uint64_t>(64, std::min<uint64_t>(ns, 4096));
-  c->nslots = (uint32_t)ns;
+  const uint32_t hcap = (uint32_t)std::min<uint64_t>(4ull * ncell + 8ull, 1ull << 16);
+  const uint64_t per_slot = (uint64_t)hcap * 8ull + ncell * 4ull;
+  if (need == 0)
+    need = std::max(astar_wave_slots(c->G, c->num_cu, true), astar_wave_slots(c->G, c->num_cu, false));
+  const uint64_t cap = std::max<uint64_t>(64, std::min<uint64_t>((32ull << 30) / per_slot, 4096));
+  const uint32_t ns = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(need, 64), cap);
+  if (c->d_heaps && ns <= c->nslots) return TSW_OK;
+  HIPCHK(hipStreamSynchronize(c->s));
+  if (c->d_heaps) HIPCHK(hipFree(c->d_heaps));
+  if (c->d_gs) HIPCHK(hipFree(c->d_gs));
+  if (c->d_epochs) HIPCHK(hipFree(c->d_epochs));
+  c->d_heaps = nullptr;
+  c->d_gs = nullptr;
+  c->d_epochs = nullptr;
+  c->nslots = 0;
+  c->hcap = hcap;
   HIPCHK(hipMalloc(&c->d_heaps, (size_t)ns * c->hcap * 8ull));
   HIPCHK(hipMalloc(&c->d_gs, (size_t)ns * ncell * 4ull));
   // every initialisation goes on the context's (non-blocking) stream: a legacy
@@ -532,6 +541,7 @@ int ensure_astar_scratch(tsw_ctx* c) {
   HIPCHK(hipMemsetAsync(c->d_gs, 0, (size_t)ns * ncell * 4ull, c->s));
   HIPCHK(hipMalloc(&c->d_epochs, (size_t)ns * 4ull));
   HIPCHK(hipMemsetAsync(c->d_epochs, 0, (size_t)ns * 4ull, c->s));
+  c->nslots = ns;
   return TSW_OK;
 }
 
@@ -1231,6 +1241,16 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.dist = c->d_dist;
   P.nbmask = c->d_nbmask;
   P.live = c->d_live;
+  {
+    // K4 32-bit keys: task ids need kshift bits with 2^kshift > m (a valid key is never 0xFFFFFFFF, the
+    // taken marker); distances saturate at DSAT = 2^(32 - kshift) - 1. Exact when DSAT exceeds every
+    // on-grid distance (W + H - 2): a key at DSAT then belongs to an off-grid pickup, and if the minimum
+    // is saturated every task left is off-grid — assigning any of them fails as the reference panics.
+    uint32_t kb = 1;
+    while (kb < 31u && (1ull << kb) <= (uint64_t)m) ++kb;
+    P.kshift = kb;
+    P.key32 = ((1ull << (32u - kb)) - 1ull) > (uint64_t)c->G.W + c->G.H ? 1u : 0u;
+  }
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;
   P.goal_tab = c->d_goal_tab;
@@ -1345,10 +1365,6 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.preempt = c->tun.chain_preempt ? 1u : 0u;
     W.avoid_xcc = c->tun.avoid_xcc ? 1u : 0u;
     W.hflags = c->d_flags;
-    W.gs_all = c->d_gs;
-    W.epochs = c->d_epochs;
-    W.heaps = c->d_heaps;
-    W.ghcap = c->hcap;
     const WorkerCfg wcfg =
         worker_config(c->G, c->num_cu, P.n, c->tun.wave_hcap, c->tun.worker_gs, c->tun.dag_exit, lds, c->tun.worker_fb);
     W.dag = wcfg.dag;
@@ -1370,6 +1386,11 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.lds_per_wave = (uint32_t)((wcfg.lds + 15u) & ~(size_t)15u);
     W.wpb = W.lds_per_wave ? (uint32_t)std::min<size_t>(block / 64u, lds / W.lds_per_wave) : 0u;
     const uint32_t want = W.wpb * (uint32_t)std::max(c->num_cu - 1, 0);
+    TRY(ensure_astar_scratch(c, want));  // one g-score / heap slot per worker wave
+    W.gs_all = c->d_gs;
+    W.epochs = c->d_epochs;
+    W.heaps = c->d_heaps;
+    W.ghcap = c->hcap;
     W.nworkers = std::min(want, c->nslots);
     P.spec_hi = 2u * W.nworkers;  // a backlog of two pairs per worker counts as keeping up
     wblocks = W.wpb ? (W.nworkers + W.wpb - 1u) / W.wpb : 0u;
@@ -1482,8 +1503,10 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       c->st.rule_rounds += k.rule_rounds;
       c->st.move_rounds += k.move_rounds;
       if (c->tun.plan_debug) {
-        unsigned long long tk[32];
+        unsigned long long tk[40];
         HIPCHK(hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[k_plan] assign us: transitions %.0f compaction %.0f scan %.0f accept %.0f update %.0f | sections %llu batches %llu accepted %llu\n",
+                tk[32] / 100.0, tk[33] / 100.0, tk[34] / 100.0, tk[35] / 100.0, tk[36] / 100.0, tk[39], tk[37], tk[38]);
         fprintf(stderr, "[k_plan] PRE1 publish us %.0f (%llu) | rules init us %.0f prefetch us %.0f publish us %.0f (%llu)\n",
                 tk[24] / 100.0, tk[25], tk[26] / 100.0, tk[27] / 100.0, tk[28] / 100.0, tk[29]);
         fprintf(stderr, "[k_plan] wave rules kcycles: load %.0f stale %.0f fast %.0f update %.0f slow %.0f rot %.0f | "
@@ -1817,8 +1840,8 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned status", e);
   if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
-  if ((e = hipMalloc(&c->d_ticks, 32 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
-  if ((e = hipMemsetAsync(c->d_ticks, 0, 32 * sizeof(unsigned long long), c->s)) != hipSuccess)
+  if ((e = hipMalloc(&c->d_ticks, 40 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
+  if ((e = hipMemsetAsync(c->d_ticks, 0, 40 * sizeof(unsigned long long), c->s)) != hipSuccess)
     return fail("memset ticks", e);
   hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, c->device);
   if (c->wall_khz <= 0) c->wall_khz = 100000;
@@ -2383,7 +2406,7 @@ int tsw_reset_stats(tsw_ctx* c) {
   const uint64_t tabs = c->st.tables;
   c->st = tsw_stats{};
   c->st.tables = tabs;
-  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 32 * sizeof(unsigned long long), c->s);
+  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 40 * sizeof(unsigned long long), c->s);
   return TSW_OK;
 }
 

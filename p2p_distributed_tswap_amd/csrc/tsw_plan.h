@@ -76,6 +76,9 @@ struct PlanArgs {
   // K4: per task its pickup point (x | y << 16, coordinates clamped to 0xFFFE) while unused, TASK_TAKEN
   // once assigned; padded with TASK_TAKEN to a multiple of 4 entries (the scan reads 16-B vectors)
   uint32_t* live;
+  // K4 keys: (min(distance, 2^(32 - kshift) - 1) << kshift) | task as one u32 when key32 (2^kshift > m and
+  // the saturation level exceeds every on-grid distance; tsw_capi.hip plan_args), else u64, one agent at a time
+  uint32_t kshift, key32;
   const uint32_t* pick;
   const uint32_t* dlv;
   const int32_t* goal_tab;

@@ -45,6 +45,7 @@ constexpr uint32_t OCC_IDX = 0x7FFFFFFFu;
 constexpr uint32_t SUCC_TERM = 0xFFFFFFFFu;
 constexpr uint32_t NO_AGENT = 0xFFFFFFFFu;
 constexpr uint32_t NO_CELL = 0xFFFFFFFFu;
+constexpr uint32_t ABATCH = 8;    // K4: idle agents whose nearest pickups one pass over the tasks computes
 constexpr uint32_t LIST_CAP = 1024;  // entries of the kernel's LDS `list` (ASSIGN compaction, changed agents)
 // movement-round decision states
 constexpr uint8_t DEC_OPEN = 0, DEC_DONE = 1, DEC_STAY = 2, DEC_MOVE = 3, DEC_SWAP = 4;
@@ -766,7 +767,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
   __shared__ uint32_t s_ap[128];  // rules: members of a rule-4 cycle rotated by the wave (<= 64), links
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
-  __shared__ unsigned long long s_tick[32], s_tlast, s_tp;
+  __shared__ uint64_t s_bestk[ABATCH];  // K4: per batch agent, block minimum of (distance, task) (LDS atomic min)
+  __shared__ uint32_t s_apos[ABATCH], s_acct[ABATCH], s_cnt2, s_bestk32[ABATCH];
+  __shared__ unsigned long long s_tick[40], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
   __shared__ uint32_t s_bad;               // ASSIGN looked up an off-grid/blocked task cell
   __shared__ uint32_t s_nassign, s_npick;  // diagnostics: this step's assignments / pickup arrivals
@@ -884,7 +887,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     s_q[4] = 0;
     s_q[5] = s_ctl.t;  // the timestep speculative entries are queued in (coop mode)
     if (P.coop) __hip_atomic_store(&P.cc->t_now, s_ctl.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int k = 0; k < 32; ++k) s_tick[k] = 0;
+    for (int k = 0; k < 40; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
     // the host's watchdog: the planner block is resident
@@ -949,7 +952,13 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       // run one after another in index order, each a block-wide argmin over the LIVE array. The first
       // agent whose delivery cell is bad (pos2id panics, :112) ends the step there: assignments of
       // agents below it still happen (and may panic first, :136), none above it.
-      if (tid == 0) s_nassign = s_npick = s_bad = 0;
+      if (tid == 0) {
+        s_nassign = s_npick = s_bad = 0;
+        if (P.dbg) {
+          s_tp = wall_clock64();
+          s_tick[39] += 1;  // diagnostics: ASSIGN sections (sub-phase ticks in [32..38])
+        }
+      }
       __syncthreads();
       const uint32_t m4 = (P.m + 3u) & ~3u;
       for (uint32_t base = 0; base < n && !s_bad; base += bd) {
@@ -986,6 +995,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         const uint64_t bal = __ballot(idle);
         if (lane == 0) s_wcount[wid] = (uint32_t)__popcll(bal);
         __syncthreads();
+        PLAN_TICK(32);
         if (idle) {
           uint32_t off = 0;
           for (uint32_t w = 0; w < wid; ++w) off += s_wcount[w];
@@ -998,28 +1008,64 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
           s_cnt = c;
         }
         __syncthreads();
+        PLAN_TICK(33);
         const uint32_t cnt = s_cnt, bad_at = s_badat;
-        for (uint32_t kk = 0; kk < cnt && !s_bad; ++kk) {
-          const uint32_t ai = list[kk];
-          if (ai > bad_at || s_ctl.unused == 0u) break;  // block-uniform: LDS values read after a barrier
-          const uint32_t v = S.V[ai];
-          const uint32_t px = v % W, py = v / W;
-          // first minimum of (Manhattan(pos, pickup), task index) over unused tasks (min_by_key, :125-130)
-          uint64_t best = ~0ull;
-          if (P.tasks_lds) {
-            for (uint32_t t = tid; t < P.m; t += bd) {
-              const uint32_t xy = S.LIVE[t];
-              const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
-              const uint32_t d = (px > tx ? px - tx : tx - px) + (py > ty ? py - ty : ty - py);
+        // Assignments in batches of up to ABATCH agents (index order): one block-wide pass computes every
+        // batch agent's first minimum over the unused tasks at once, then thread 0 accepts them in agent
+        // order up to the first agent whose task an earlier agent of the batch took (that agent and the
+        // rest re-run in the next batch, against the updated LIVE array). An accepted agent's minimum was
+        // taken over a superset of what was unused at its sequential turn and its task is still unused,
+        // so it IS the sequential first minimum (min_by_key, tswap.rs:125-130).
+        // batch size adapts: it doubles after a batch without a conflict and drops to the accepted count
+        // after one (the t = 0 burst of a dense instance conflicts often; a busy step's handful rarely)
+        uint32_t bcur = ABATCH;
+        for (uint32_t kk = 0; kk < cnt && !s_bad;) {
+          const uint32_t B = min(bcur, cnt - kk);
+          if (tid < B) {
+            const uint32_t v = S.V[list[kk + tid]];
+            s_apos[tid] = (v % W) | ((v / W) << 16);
+            s_bestk[tid] = ~0ull;
+            s_bestk32[tid] = 0xFFFFFFFFu;
+          }
+          __syncthreads();
+          // One 32-bit key per batch agent and thread: (min(distance, DSAT) << kshift) | task — comparable
+          // across threads, reduced with the DPP wave min; the batch agents' cells sit in SGPRs
+          // (block-uniform). A taken task's key is all ones and never wins. Without 32-bit keys
+          // (P.key32 == 0: huge task sets or grids) one agent per batch with 64-bit keys.
+          const uint32_t q4 = m4 >> 2;
+          const bool k32 = P.key32 != 0u;
+          const uint32_t ksh = P.kshift, dsat = (uint32_t)((1ull << (32u - ksh)) - 1ull);
+          uint32_t apos[ABATCH], best[ABATCH];
+#pragma unroll
+          for (uint32_t b = 0; b < ABATCH; ++b) {
+            apos[b] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b < B ? s_apos[b] : 0u));
+            best[b] = 0xFFFFFFFFu;
+          }
+          uint64_t best64 = ~0ull;  // !k32: agent 0 only
+          auto visit = [&](uint32_t xy, uint32_t t) {
+            const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
+            if (k32) {
+              const uint32_t tk = (xy == TASK_TAKEN ? 0xFFFFFFFFu : 0u) | t;
+#pragma unroll
+              for (uint32_t b = 0; b < ABATCH; ++b) {
+                if (b >= B) break;  // block-uniform
+                const uint32_t d = __usad(apos[b] & 0xFFFFu, tx, __usad(apos[b] >> 16, ty, 0u));  // v_sad_u32
+                best[b] = min(best[b], (min(d, dsat) << ksh) | tk);
+              }
+            } else {
+              const uint32_t d = __usad(apos[0] & 0xFFFFu, tx, __usad(apos[0] >> 16, ty, 0u));
               const uint64_t key = xy == TASK_TAKEN ? ~0ull : (((uint64_t)d << 32) | t);
-              best = key < best ? key : best;
+              best64 = key < best64 ? key : best64;
             }
+          };
+          const uint32_t Bs = k32 ? B : 1u;
+          if (P.tasks_lds) {
+            for (uint32_t t = tid; t < P.m; t += bd) visit(S.LIVE[t], t);
           } else {
-            // 16-B vectors, lane-interleaved (one coalesced 1 KB read per wave per vector), up to eight in
-            // flight per lane: C3's 32,000 tasks are one pass of eight loads per lane
-            const uint4* L4 = reinterpret_cast<const uint4*>(S.LIVE);
-            const uint32_t q4 = m4 >> 2;
-            constexpr uint32_t VL = 8u;
+            // 16-B vectors from global memory (P.live: global loads, not flat), lane-interleaved — one
+            // coalesced 1 KB read per wave per vector — four in flight
+            const uint4* L4 = reinterpret_cast<const uint4*>(P.live);
+            constexpr uint32_t VL = 4u;
             for (uint32_t j0 = tid; j0 < q4; j0 += VL * bd) {
               uint4 a[VL];
 #pragma unroll
@@ -1027,46 +1073,78 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                 a[u] = j0 + u * bd < q4 ? L4[j0 + u * bd] : make_uint4(TASK_TAKEN, TASK_TAKEN, TASK_TAKEN, TASK_TAKEN);
 #pragma unroll
               for (uint32_t u = 0; u < VL; ++u) {
-                const uint32_t xs[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+                const uint32_t t4 = (j0 + u * bd) * 4u;
+                visit(a[u].x, t4);
+                visit(a[u].y, t4 + 1u);
+                visit(a[u].z, t4 + 2u);
+                visit(a[u].w, t4 + 3u);
+              }
+            }
+          }
+          if (k32) {
 #pragma unroll
-                for (uint32_t e = 0; e < 4u; ++e) {
-                  const uint32_t xy = xs[e];
-                  const uint32_t t = (j0 + u * bd) * 4u + e;
-                  const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
-                  const uint32_t d = (px > tx ? px - tx : tx - px) + (py > ty ? py - ty : ty - py);
-                  const uint64_t key = xy == TASK_TAKEN ? ~0ull : (((uint64_t)d << 32) | t);
-                  best = key < best ? key : best;
-                }
-              }
+            for (uint32_t b = 0; b < ABATCH; ++b) {
+              if (b >= B) break;  // block-uniform
+              const uint32_t wm = __ockl_wfred_min_u32(best[b]);
+              if (lane == 0 && wm != 0xFFFFFFFFu) atomicMin(&s_bestk32[b], wm);
             }
+          } else {
+            const uint64_t wm = wave_min_u64(best64);
+            if (lane == 0 && wm != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(&s_bestk[0]), wm);
           }
-          best = wave_min_u64(best);
-          if (lane == 0) s_red[wid] = best;
           __syncthreads();
+          PLAN_TICK(34);
           if (tid == 0) {
-            uint64_t b = ~0ull;
-            for (uint32_t w = 0; w < nwaves; ++w) b = s_red[w] < b ? s_red[w] : b;
-            if (b != ~0ull) {  // first minimum (min_by_key, tswap.rs:130)
-              const uint32_t t = (uint32_t)(b & 0xFFFFFFFFu);
-              S.LIVE[t] = TASK_TAKEN;
-              if (P.tasks_lds) P.live[t] = TASK_TAKEN;
-              s_ctl.unused -= 1u;
-              P.task[ai] = (int32_t)t;
-              P.st[ai] = ST_TO_PICKUP;
-              ++s_nassign;
-              if (P.dbg) S.DEC[ai] = 0x40;
-              const uint32_t ng = P.pick[t];
-              if (ng == CELL_BAD) {  // pos2id[&task.pickup] panics (tswap.rs:136)
-                atomicOr(&P.ctl->err, ERR_BAD_PICKUP);
-                s_bad = 1;
-              } else {
-                S.G[ai] = ng;
-                S.GT[ai] = P.goal_tab[ng];
-                S.NHC[ai] = NHC_DIRTY;
+            uint32_t acc = 0, stop = 0;
+            const uint32_t Bk = P.key32 ? B : 1u;
+            if (P.key32)  // 32-bit keys -> (distance, task) as the u64 path has them
+              for (uint32_t b = 0; b < Bk; ++b)
+                s_bestk[b] = s_bestk32[b] == 0xFFFFFFFFu ? ~0ull : (uint64_t)(s_bestk32[b] & ((1u << P.kshift) - 1u));
+            for (uint32_t b = 0; b < Bk; ++b) {
+              if (list[kk + b] > bad_at || s_ctl.unused == 0u || s_bestk[b] == ~0ull) {
+                stop = 1;  // past the first bad delivery / out of tasks: this step assigns no more
+                break;
               }
+              const uint32_t t = (uint32_t)(s_bestk[b] & 0xFFFFFFFFu);
+              bool taken = false;
+              for (uint32_t e = 0; e < acc; ++e) taken |= s_acct[e] == t;
+              if (taken) break;  // conflict: this agent re-runs in the next batch
+              s_acct[acc++] = t;
+              s_ctl.unused -= 1u;
+            }
+            s_cnt2 = acc;
+            s_doit = stop;
+            s_nassign += acc;
+            if (P.dbg) {
+              s_tick[37] += 1;    // batches
+              s_tick[38] += acc;  // agents accepted
             }
           }
           __syncthreads();
+          PLAN_TICK(35);
+          const uint32_t acc = s_cnt2;
+          if (tid < acc) {  // the accepted agents' updates in parallel (tswap.rs:132-136)
+            const uint32_t ai = list[kk + tid], t = s_acct[tid];
+            S.LIVE[t] = TASK_TAKEN;
+            if (P.tasks_lds) P.live[t] = TASK_TAKEN;
+            P.task[ai] = (int32_t)t;
+            P.st[ai] = ST_TO_PICKUP;
+            if (P.dbg) S.DEC[ai] = 0x40;
+            const uint32_t ng = P.pick[t];
+            if (ng == CELL_BAD) {  // pos2id[&task.pickup] panics (tswap.rs:136)
+              atomicOr(&P.ctl->err, ERR_BAD_PICKUP);
+              s_bad = 1;
+            } else {
+              S.G[ai] = ng;
+              S.GT[ai] = P.goal_tab[ng];
+              S.NHC[ai] = NHC_DIRTY;
+            }
+          }
+          __syncthreads();
+          PLAN_TICK(36);
+          if (s_doit) break;  // block-uniform
+          kk += acc;
+          bcur = acc == B ? min(ABATCH, 2u * bcur) : max(acc, 1u);
         }
         if (bad_at != NO_AGENT && !s_bad) {  // block-uniform
           if (tid == 0) {
@@ -1428,8 +1506,9 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
             bool f = false, onck = false;
             uint64_t m = 0;
             bool pv = false;  // precomputed swap valid
-            uint32_t p_vs = 0, p_gs = 0, p_gk = 0, p_ns = SUCC_TERM;
+            uint32_t p_vs = 0, p_gs = 0, p_gk = 0, p_ns = SUCC_TERM, p_nk = SUCC_TERM;
             int32_t p_ts = -1, p_tk = -1;
+            // bits 0-7: s's new next-hop code; rule-4 2-cycle: bits 8-15 k's new code, bit 16 set
             uint32_t p_code = NH_UNKNOWN;
             bool p_fsv = false, p_walk = false;
             auto precompute = [&](bool want) {
@@ -1442,10 +1521,26 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               p_tk = S.GT[k];
               const uint32_t vk = S.V[k];
               uint32_t code = S.CANDC[k];
-              bool ok = p_vs == p_gs && vk != p_gs;  // rule 3 without a shared start cell
+              const bool r3 = p_vs == p_gs;
+              // rule 4 on a 2-cycle k <-> s (two agents meeting head on, the common firing in 1-wide aisles):
+              // the rotation (tswap.rs:241-249) is the exchange of their goals, and each one's new next hop is
+              // the other's CANDC — the code of (the cell it sits on, the goal it takes)
+              const bool r2 = !r3 && onck && S.SUCC[sk] == k;
+              bool ok = (r3 && vk != p_gs) || r2;  // rule 3 without a shared start cell, or the 2-cycle
               if (ok && code > NH_STAY) code = p_tk >= 0 ? nh_code(P, p_tk, p_vs) : NH_UNKNOWN;
               ok = ok && code <= NH_STAY;
-              p_code = code;
+              uint32_t code2 = 0, nk = SUCC_TERM;
+              if (ok && r2) {
+                code2 = S.CANDC[sk];
+                if (code2 > NH_STAY) code2 = p_ts >= 0 ? nh_code(P, p_ts, vk) : NH_UNKNOWN;
+                ok = code2 <= NH_STAY;
+                if (ok && vk != p_gs) {  // k's new successor (k takes s's goal; at it when vk == p_gs)
+                  const uint32_t oc = S.OCC[step_cell(vk, code2, W)];
+                  nk = oc == OCC_NONE ? SUCC_TERM : (oc & OCC_IDX);
+                }
+              }
+              p_code = code | (code2 << 8) | (r2 ? 0x10000u : 0u);
+              p_nk = nk;
               uint32_t ns = SUCC_TERM;
               if (ok && p_vs != p_gk) {
                 const uint32_t oc = S.OCC[step_cell(p_vs, code, W)];
@@ -1453,7 +1548,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               }
               p_ns = ns;
               p_fsv = ok && ns != SUCC_TERM && ns != sk && S.V[ns] == S.G[ns];
-              p_walk = ok && ns != SUCC_TERM && ns != sk && !p_fsv;  // s's new successor moves: cycle check
+              // s's new successor moves: cycle check; a 2-cycle rotation always walks (never batched)
+              p_walk = ok && (r2 || (ns != SUCC_TERM && ns != sk && !p_fsv));
               pv = ok;
             };
             // diagnostics (TSW_PLAN_DEBUG): shader cycles per part of the loop -> s_tick[16..23]
@@ -1585,9 +1681,12 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               uint32_t r_fl = 0, r_s = 0, r_ns = 0, r_bits = 0;
               const bool fast = __builtin_amdgcn_readlane((int)(pv ? 1u : 0u), (int)l) != 0;
               if (fast) {
-                // rule 3 (tswap.rs:198-202) from registers: b <-> s goals, s's new code and successor
+                // rule 3 (tswap.rs:198-202) from registers: b <-> s goals, s's new code and successor;
+                // a rule-4 rotation of the 2-cycle b <-> s (:241-249) is the same exchange plus b's new
+                // code and successor, and both leave the broken cycle
                 if (lane == l) {
                   const uint32_t s = sk;
+                  const bool r2 = (p_code >> 16) != 0u;
                   S.G[b] = p_gs;
                   S.GT[b] = p_ts;
                   S.G[s] = p_gk;
@@ -1596,15 +1695,28 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                   S.CANDC[b] = NHC_DIRTY;
                   S.NHC[s] = (uint8_t)p_code;
                   S.SUCC[s] = p_ns;
+                  if (r2) {
+                    S.NHC[b] = (uint8_t)(p_code >> 8);
+                    S.SUCC[b] = p_nk;
+                    S.ONC[b] = 0;
+                    S.ONC[s] = 0;
+                    if (P.dbg) s_tick[11] += 1;  // diagnostics: rule-4 rotations
+                  }
                   s_best = b;
                   s_miss = 0;
                   s_ctl.i = b + 1;
                   bool fs = p_fsv;
-                  if (p_ns != SUCC_TERM && p_ns != s && !p_fsv) {
-                    // new cycle through s? (as in fire(): a labelled agent or a self-loop ends it)
-                    uint32_t x = p_ns;
+                  // new cycles pass through an agent whose successor changed: s (both firings) and b
+                  // (rotation). A labelled agent lies on a standing cycle that contains neither, and a
+                  // self-loop is a chain end: neither leads back.
+                  const uint32_t starts[2] = {s, b};
+                  for (uint32_t w = 0; w < (r2 ? 2u : 1u); ++w) {
+                    const uint32_t st = starts[w];
+                    const uint32_t first = S.SUCC[st];
+                    if (S.ONC[st] || first == SUCC_TERM || first == st || (w == 0u && !r2 && p_fsv)) continue;
+                    uint32_t x = first;
                     uint32_t it = 0;
-                    for (; it < n && x != SUCC_TERM && x != s; ++it) {
+                    for (; it < n && x != SUCC_TERM && x != st; ++it) {
                       const uint32_t nx = S.SUCC[x];
                       if (S.ONC[x] || nx == x) {
                         x = SUCC_TERM;
@@ -1613,19 +1725,19 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                       x = nx;
                     }
                     if (P.dbg) s_tick[9] += it;
-                    if (x == s) {
-                      uint32_t y = s;
+                    if (x == st) {
+                      uint32_t y = st;
                       do {
                         S.ONC[y] = 1;
                         y = S.SUCC[y];
-                      } while (y != s);
+                      } while (y != st);
                       r_fl = FO_RESCAN;
                     }
-                    fs = false;
                   }
+                  if (r_fl) fs = false;
                   r_s = s;
                   r_ns = p_ns;
-                  r_bits = (fs ? 1u : 0u) | (p_vs == p_gk ? 4u : 0u);
+                  r_bits = (fs ? 1u : 0u) | (r2 && S.V[b] == p_gs ? 2u : 0u) | (p_vs == p_gk ? 4u : 0u);
                 }
                 // b and s joined the changed list (targeted prefetch at the phase end / next relabel)
                 const uint32_t fsx = (uint32_t)__builtin_amdgcn_readlane((int)r_s, (int)l);
@@ -1744,6 +1856,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               if (k == fs_) {
                 sk = fns;
                 f = (fbits & 1u) != 0;
+                onck = false;  // s is on no cycle now (a new one rescans)
               } else if (sk != SUCC_TERM && sk != k) {
                 if (sk == fs_) f = (fbits & 4u) != 0 || onck;
                 else if (sk == b) f = (fbits & 2u) != 0 || onck;
@@ -2135,7 +2248,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     P.ctl->err |= err;
     s_tick[s_tsec] += wall_clock64() - s_tlast;
     if (P.sec_ticks)
-      for (int k = 0; k < 32; ++k) P.sec_ticks[k] += s_tick[k];
+      for (int k = 0; k < 40; ++k) P.sec_ticks[k] += s_tick[k];
   }
 }
 

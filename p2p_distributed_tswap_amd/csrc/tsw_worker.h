@@ -327,12 +327,19 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
       if (w_ld(&A.cc->t_now) - w_ld(e + 3) > A.stale_steps) {
         uint32_t* wp = reinterpret_cast<uint32_t*>((uintptr_t)(A.nh + (uint64_t)tab * A.nstride + v) & ~(uintptr_t)3u);
         const uint32_t sh = 8u * (uint32_t)((uintptr_t)(A.nh + (uint64_t)tab * A.nstride + v) & 3u);
+        bool reset = false;
         for (;;) {
           const uint32_t w = w_ld(wp);
           if (((w >> sh) & 0xFFu) != NH_PENDING_S) break;  // resolved, promoted or reset already
-          if (w_cas(wp, w, w | (0xFFu << sh))) break;     // NH_UNKNOWN = 0xFF
+          if (w_cas(wp, w, w | (0xFFu << sh))) {           // NH_UNKNOWN = 0xFF
+            reset = true;
+            break;
+          }
         }
-        __hip_atomic_fetch_add(&A.cc->spec_dropped, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // only a reset is a drop; a code resolved meanwhile needs no work and a promoted one
+        // sits on the needed queue, so the entry is skipped either way and counted as such
+        if (reset) __hip_atomic_fetch_add(&A.cc->spec_dropped, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_fetch_add(&A.cc->qskip[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         drop = true;
       }
     }

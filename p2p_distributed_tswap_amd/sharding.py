@@ -111,10 +111,16 @@ class ShardedK3:
     """The collective half of the protocol. `codes_fn(start, goal) -> u8 codes` answers this rank's
     pairs (Planner.next_hop_codes on MI355X; the oracle in the CPU gloo tests)."""
 
+    # a rank whose codes_fn failed contributes this to the all-reduce: it wins the MIN, so every rank
+    # learns of the failure from the same collective and the protocol stays in step (ADVICE r4)
+    FAILED = -1
+
     def __init__(self, rank: int, world: int, dist, device, codes_fn):
         self.rank, self.world, self.dist, self.device, self.codes_fn = rank, world, dist, device, codes_fn
         self.stops = 0
         self.pairs = 0
+        self.local_error = None   # this rank's codes_fn exception (first one)
+        self.failed_stops = 0     # stops whose all-reduce carried FAILED
 
     def _bcast(self, arr: np.ndarray, dtype, n: int):
         import torch
@@ -134,25 +140,46 @@ class ShardedK3:
         pairs = np.concatenate([start, goal]).astype(np.int32) if self.rank == 0 else None
         pairs = self._bcast(pairs, torch.int32, 2 * k).astype(np.uint32)
         st, gl = pairs[:k], pairs[k:]
-        mine = _codes_for_rank(st, gl, self.rank, self.world, self.codes_fn)
-        # u8 codes ride in an int32 tensor (MIN over ranks: the owner's code, others 0xFF)
-        t = torch.from_numpy(mine.astype(np.int32)).to(self.device)
+        try:
+            mine = _codes_for_rank(st, gl, self.rank, self.world, self.codes_fn).astype(np.int32)
+        except Exception as e:  # noqa: BLE001 — reported after the collective, on every rank
+            if self.local_error is None:
+                self.local_error = e
+            mine = np.full(k, self.FAILED, dtype=np.int32)
+        # u8 codes ride in an int32 tensor (MIN over ranks: the owner's code, others 0xFF; FAILED wins)
+        t = torch.from_numpy(mine).to(self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
         self.stops += 1
         self.pairs += k
-        return t.cpu().numpy().astype(np.uint8)
+        return t.cpu().numpy()
+
+    def _failure(self) -> RuntimeError:
+        if self.local_error is not None:
+            return RuntimeError(f"sharded K3: rank {self.rank}'s next-hop codes failed: {self.local_error}")
+        return RuntimeError("sharded K3: another rank's next-hop codes failed")
 
     def resolve(self, start: np.ndarray, goal: np.ndarray) -> np.ndarray:
-        """Rank 0's resolver (one planner stop)."""
+        """Rank 0's resolver (one planner stop). Raises (after the stop's collectives completed on every
+        rank) when any rank failed to answer; the plan then fails and finish() releases the servers."""
         codes = self._exchange(start, goal)
+        if np.any(codes == self.FAILED):
+            self.failed_stops += 1
+            raise self._failure()
         if np.any(codes > 4):
             raise RuntimeError("a next hop was answered by no rank")
-        return codes
+        return codes.astype(np.uint8)
 
     def serve(self) -> None:
-        """Ranks > 0: answer stops until rank 0's plan ends (finish())."""
-        while self._exchange(np.zeros(0, np.uint32), np.zeros(0, np.uint32)) is not None:
-            pass
+        """Ranks > 0: answer stops until rank 0's plan ends (finish()). A stop that failed anywhere does
+        not end the loop — rank 0 still sends finish() — and is raised here afterwards."""
+        while True:
+            codes = self._exchange(np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+            if codes is None:
+                break
+            if np.any(codes == self.FAILED):
+                self.failed_stops += 1
+        if self.failed_stops:
+            raise self._failure()
 
     def finish(self) -> None:
         """Rank 0: release the serving ranks."""

@@ -106,3 +106,47 @@ def test_goal_owner_partition():
     g = np.arange(50, dtype=np.uint32)
     own = sharding.goal_owner(g, 4)
     assert set(own.tolist()) == {0, 1, 2, 3} and np.array_equal(own, g % 4)
+
+
+def _failing_worker(rank, world, port, q, bad_rank):
+    """Rank `bad_rank`'s codes_fn raises on the third stop it answers: every rank must leave the protocol
+    with an error (no rank left blocked in a collective) — ADVICE r4."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = [0]
+
+    def codes(start, goal):
+        calls[0] += 1
+        if rank == bad_rank and calls[0] >= 3:
+            raise ValueError("injected failure")
+        return np.full(start.size, 4, dtype=np.uint8)
+
+    def plan(resolve):
+        for _ in range(10):  # ten stops of 8 pairs; goals cover every owner
+            resolve(np.arange(8, dtype=np.uint32), np.arange(8, dtype=np.uint32) + 100)
+        return "done"
+
+    outcome = "ok"
+    try:
+        sharding.plan_sharded_k3(rank, world, dist, "cpu", codes, plan)
+    except RuntimeError as e:
+        outcome = "injected" if "injected failure" in str(e) else "other-rank"
+    q.put((rank, outcome))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad_rank", [0, 1])
+def test_sharded_k3_failing_rank_does_not_deadlock(bad_rank):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, q, bad_rank)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[bad_rank] == "injected"
+    assert res[1 - bad_rank] == "other-rank"
