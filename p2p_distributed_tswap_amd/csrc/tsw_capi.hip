@@ -68,6 +68,7 @@ struct Tunables {
   uint32_t wave_rules_max = 0xFFFFFFFFu;  // TSW_WAVE_RULES_MAX: wave-0 rules rounds when n <= this
   uint32_t wide_prefetch = 8;     // TSW_WIDE_PREFETCH: resolved hops walked ahead (0 = candidates only)
   uint32_t wide_hi = 16, wide_lo = 4;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops with a small / large speculative backlog
+  uint32_t dag_width = 4;         // TSW_DAG_WIDTH: cells per DAG prefetch level (<= 16)
   uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
   uint32_t prefetch_ext = 7;      // TSW_PREFETCH_EXT: bit 0 DAG from an agent's own unresolved cell, bit 1 walk past the pickup, bit 2 walk-ahead for agents a firing changed (C3 476 -> 409 ms with bits 0-1)
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
@@ -83,6 +84,8 @@ struct Tunables {
   int worker_fb = -1;             // TSW_WORKER_FB=0 / 1: global-g-score workers without / with the staged free bitmap (-1: by waves per CU)
   bool dag_exit = true;           // TSW_DAG_EXIT=0: coop workers' A* runs to the goal's pop (no DAG early exit)
   uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
+  uint32_t ab_flags = 0;          // TSW_AB_FLAGS (A/B): 1 no 2-cycle fast path, 2 no end-of-rules prefetch, 4 one agent per K4 batch
+  uint32_t t0_delay_us = 0;       // TSW_T0_DELAY_US (A/B): the planner idles this long after step 0's assignment
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
   uint32_t reg_heap = 63;         // TSW_ASTAR_REGHEAP: worker A* heaps up to this many entries in registers (0: LDS only)
   // idle-worker polling (tsw_worker.h worker_claim; profiles/r4/poll_ab.txt: C3 371-383 -> 355 ms)
@@ -121,6 +124,9 @@ struct Tunables {
     t.wide_hi = (uint32_t)num("TSW_WIDE_HI", 0, 1 << 16, t.wide_hi);
     t.wide_lo = (uint32_t)num("TSW_WIDE_LO", 1, 1 << 16, t.wide_lo);
     t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 16, t.dag_prefetch);
+    t.dag_width = (uint32_t)num("TSW_DAG_WIDTH", 1, 16, t.dag_width);
+    t.ab_flags = (uint32_t)num("TSW_AB_FLAGS", 0, 255, t.ab_flags);
+    t.t0_delay_us = (uint32_t)num("TSW_T0_DELAY_US", 0, 10000000, t.t0_delay_us);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
     t.part_lds = (uint32_t)num("TSW_PART_LDS", 0, 0x7F, t.part_lds);
@@ -246,6 +252,8 @@ struct tsw_ctx {
   PlanCtl* d_ctl = nullptr;
   PlanCtl* h_ctl = nullptr;      // pinned
   unsigned long long* d_ticks = nullptr;
+  uint32_t* d_dtag = nullptr;  // TSW_PLAN_DEBUG: per-agent change tags (PlanArgs::dtag)
+  uint32_t dtag_cap = 0;
   int wall_khz = 100000;
   uint32_t chase_id = 0;
 
@@ -1187,16 +1195,23 @@ int ensure_agents(tsw_ctx* c, size_t n) {
 
 // Coop-mode buffers: control block, speculative queue, the needed queue sized for a whole launch,
 // the second stream and the host-visible "planner resident" flag.
-int ensure_coop(tsw_ctx* c, uint32_t n) {
+int ensure_coop(tsw_ctx* c, uint32_t n, uint32_t max_t = 0) {
   TRY(ensure_astar_scratch(c));
   TRY(ensure_queue(c, std::max<size_t>(4 * (size_t)n + 4096, (size_t)1 << 18)));
   if (!c->d_cc) {
     HIPCHK(hipMalloc(&c->d_cc, sizeof(CoopCtl)));
     HIPCHK(hipHostMalloc(&c->h_cc, sizeof(CoopCtl), hipHostMallocDefault));
   }
-  if (!c->d_QS) {
+  // The speculative queue is linear over a plan launch (the planner appends, the workers claim in
+  // order): once it is full the planner stops speculating for the rest of the launch. C5 (10,000 agents,
+  // 2,001 steps) queues ~1M pairs, exactly the old fixed 2^20 entries: the queue filled up mid-plan and
+  // every later step waited on unprefetched pairs (43 s instead of 8 s). Sized by the plan: half an entry
+  // per agent-step, 2^20 .. 2^26 entries (16 MB .. 1 GB of HBM).
+  const size_t want_qs = std::min<size_t>(std::max<size_t>((size_t)n * (max_t + 1u) / 2u, (size_t)1 << 20),
+                                          (size_t)1 << 26);
+  if (!c->d_QS || c->qscap < want_qs) {
     HIPCHK(hipStreamSynchronize(c->s));
-    HIPCHK(dgrow(c->d_QS, c->qscap, (size_t)1 << 20));
+    HIPCHK(dgrow(c->d_QS, c->qscap, want_qs));
   }
   return TSW_OK;
 }
@@ -1237,6 +1252,9 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.wide_lo = c->tun.wide_lo;
   P.spec_hi = 0;  // set per launch from the worker count (run_plan_impl)
   P.dag_prefetch = c->tun.dag_prefetch;
+  P.dag_width = c->tun.dag_width;
+  P.ab_flags = c->tun.ab_flags;
+  P.t0_delay_ticks = c->tun.t0_delay_us * 100u;
   P.prefetch_ext = c->tun.prefetch_ext;
   P.dist = c->d_dist;
   P.nbmask = c->d_nbmask;
@@ -1263,6 +1281,16 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.ctl = c->d_ctl;
   P.sec_ticks = c->d_ticks;
   P.dbg = c->tun.plan_debug ? 1u : 0u;
+  P.dtag = nullptr;
+  if (P.dbg && n) {  // diagnostics only: per-agent change tags
+    if (c->dtag_cap < n) {
+      if (c->d_dtag) (void)hipFree(c->d_dtag);
+      c->d_dtag = nullptr;
+      c->dtag_cap = 0;
+      if (hipMalloc(&c->d_dtag, (size_t)n * 4) == hipSuccess) c->dtag_cap = n;
+    }
+    if (c->d_dtag && hipMemsetAsync(c->d_dtag, 0, (size_t)n * 4, c->s) == hipSuccess) P.dtag = c->d_dtag;
+  }
   // LDS residency, in priority order: agents, occupancy grid, task table
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
@@ -1523,6 +1551,20 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                   "MOVE %u/%u | PRE1 never queued: assigned %u, picked up %u | chain queries %llu of %llu\n", cc.dbg_need[0], cc.dbg_need[1], cc.dbg_need[2],
                   cc.dbg_need[3], cc.dbg_need[4], cc.dbg_need[5], cc.dbg_need[6], cc.dbg_need[7],
                   (unsigned long long)cc.chain_queries, (unsigned long long)cc.worker_queries);
+          {
+            static const char* nm[6] = {"r3b", "r3s", "rot", "mv", "asg", "pick"};
+            std::string line = "[k_plan] PRE1 unresolved by agent change (unknown/pending):";
+            for (int tg = 0; tg < 64; ++tg) {
+              if (!cc.dbg_tag[0][tg] && !cc.dbg_tag[1][tg]) continue;
+              std::string name;
+              for (int b = 0; b < 6; ++b)
+                if (tg & (1 << b)) name += (name.empty() ? "" : "+") + std::string(nm[b]);
+              char buf[96];
+              snprintf(buf, sizeof buf, " %s %u/%u", name.empty() ? "none" : name.c_str(), cc.dbg_tag[0][tg], cc.dbg_tag[1][tg]);
+              line += buf;
+            }
+            fprintf(stderr, "%s\n", line.c_str());
+          }
           fprintf(stderr, "[k_plan] speculative pairs dropped as stale: %u (older than %u timesteps)\n",
                   cc.spec_dropped, c->tun.stale_steps);
           fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u | queue delay enqueue -> claim: needed "
@@ -1656,7 +1698,7 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   TRY(ensure_queue(c, 4 * (size_t)n + 4096));  // needed pairs (<= 2n per exit) + speculative prefetch (qcap/2)
   c->qt_count = 0;
   if (c->tun.coop && !c->resolver && !eager_policy(c, 0)) {
-    TRY(ensure_coop(c, n));
+    TRY(ensure_coop(c, n, max_t));
     if (c->tun.task_chains && m) {
       // every task's pickup -> delivery path, resolved hop by hop by the workers in the background
       // (lowest priority): an agent that picks the task up finds its next hops already there
@@ -1872,7 +1914,7 @@ void tsw_destroy(tsw_ctx* c) {
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
   fre(c->d_gt); fre(c->d_dec); fre(c->d_mu); fre(c->d_dups); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
   if (c->h_dups) (void)hipHostFree(c->h_dups);
-  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_live); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
+  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_dtag); fre(c->d_live); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
   fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
   if (c->h_cc) (void)hipHostFree(c->h_cc);

@@ -98,6 +98,10 @@ struct CoopCtl {
   uint32_t t_now;
   uint32_t spec_dropped;  // ... entries dropped that way
   uint32_t pad4;
+  // diagnostics (TSW_PLAN_DEBUG): PRE1 agents whose pair was unresolved after the step-start refresh, by
+  // what changed them since the previous PRE1 (PlanArgs::dtag bits: 1 rule-3 b, 2 rule-3 s, 4 rotated,
+  // 8 moved, 16 assigned, 32 picked up), [0] unknown / [1] pending-speculative per tag combination
+  uint32_t dbg_tag[2][64];
 };
 
 struct AstarQuery {

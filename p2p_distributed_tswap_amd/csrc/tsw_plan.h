@@ -55,6 +55,9 @@ struct PlanArgs {
   uint32_t wide_hi, wide_lo;    // coop mode: step-start walk-ahead hops when the speculative backlog is small / large
   uint32_t spec_hi;             // coop mode: backlog (queued, unclaimed speculative pairs) counted as small up to this
   uint32_t dag_prefetch;        // walk-ahead also queues the shortest-path successors of the first unresolved cell
+  uint32_t dag_width;           // ... at most this many cells per DAG level (0: 4)
+  uint32_t ab_flags;            // diagnostic A/B switches (Tunables::ab_flags; 0 in the product build)
+  uint32_t t0_delay_ticks;      // diagnostic: idle after step 0's assignment (100 MHz ticks)
   uint32_t prefetch_ext;        // bit 0: DAG from an agent's own unresolved cell; bit 1: walk on past the pickup
   const uint16_t* dist;         // K1 distance tables (nstride entries per slot), for dag_prefetch
   const uint8_t* nbmask;        // per cell: bit d = neighbour in direction d is free
@@ -91,6 +94,7 @@ struct PlanArgs {
   PlanCtl* ctl;
   unsigned long long* sec_ticks;  // [16] wall-clock ticks per section [0..7] and sub-phase [8..15] (diagnostics)
   uint32_t dbg;                   // sub-phase ticks on (TSW_PLAN_DEBUG)
+  uint32_t* dtag;                 // diagnostics (TSW_PLAN_DEBUG): per agent, what changed it since PRE1 (CoopCtl::dbg_tag)
   // coop mode: K3 runs concurrently in the dispatch's worker workgroups (tsw_worker.h); Q is the needed queue (qcap entries for the
   // whole launch), QS the speculative one; missing next hops are waited for instead of exiting
   uint32_t coop;

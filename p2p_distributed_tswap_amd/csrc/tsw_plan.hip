@@ -587,7 +587,8 @@ __device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t
 // capped at DAG_WIDTH; a resolved cell contributes only the cell its code points at), so a path
 // resolves several cells per A* latency instead of one.
 __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab) {
-  constexpr uint32_t DAG_WIDTH = 4;
+  constexpr uint32_t DAG_WIDTH = 16;  // array bound; P.dag_width caps the frontier (default 4)
+  const uint32_t dwid = P.dag_width ? min(P.dag_width, DAG_WIDTH) : 4u;
   const uint16_t* dt = P.dist + (uint64_t)tab * P.nstride;
   const uint8_t* ht = P.nh + (uint64_t)tab * P.nstride;
   uint32_t fr[DAG_WIDTH], nf = 1;
@@ -597,7 +598,7 @@ __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint3
     auto add = [&](uint32_t w) {
       for (uint32_t i = 0; i < nn; ++i)
         if (nx[i] == w) return;
-      if (nn < DAG_WIDTH) nx[nn++] = w;
+      if (nn < dwid) nx[nn++] = w;
     };
     for (uint32_t i = 0; i < nf; ++i) {
       const uint32_t x = fr[i];
@@ -736,6 +737,11 @@ __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
 }  // namespace
 
 // diagnostics: wall-clock ticks of sub-phases (P.sec_ticks[8..15], printed by TSW_PLAN_DEBUG)
+#define DTAG(k, bits)                                        \
+  do {                                                       \
+    if (P.dbg && P.dtag) atomicOr(&P.dtag[(k)], (uint32_t)(bits)); \
+  } while (0)
+
 #define PLAN_TICK(slot)                              \
   do {                                               \
     if (P.dbg && tid == 0) {                         \
@@ -973,6 +979,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               st = ST_TO_DELIVERY;
               atomicAdd(&s_npick, 1u);
               if (P.dbg) S.DEC[i] = 0x41;  // diagnostics tag (MOVE re-initialises DEC)
+              DTAG(i, 32u);
               const int32_t tk = P.task[i];
               if (tk >= 0) {
                 const uint32_t ng = P.dlv[tk];
@@ -1018,7 +1025,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         // so it IS the sequential first minimum (min_by_key, tswap.rs:125-130).
         // batch size adapts: it doubles after a batch without a conflict and drops to the accepted count
         // after one (the t = 0 burst of a dense instance conflicts often; a busy step's handful rarely)
-        uint32_t bcur = ABATCH;
+        uint32_t bcur = (P.ab_flags & 4u) ? 1u : ABATCH;
         for (uint32_t kk = 0; kk < cnt && !s_bad;) {
           const uint32_t B = min(bcur, cnt - kk);
           if (tid < B) {
@@ -1130,6 +1137,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
             P.task[ai] = (int32_t)t;
             P.st[ai] = ST_TO_PICKUP;
             if (P.dbg) S.DEC[ai] = 0x40;
+            DTAG(ai, 16u);
             const uint32_t ng = P.pick[t];
             if (ng == CELL_BAD) {  // pos2id[&task.pickup] panics (tswap.rs:136)
               atomicOr(&P.ctl->err, ERR_BAD_PICKUP);
@@ -1144,7 +1152,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
           PLAN_TICK(36);
           if (s_doit) break;  // block-uniform
           kk += acc;
-          bcur = acc == B ? min(ABATCH, 2u * bcur) : max(acc, 1u);
+          bcur = (P.ab_flags & 4u) ? 1u : acc == B ? min(ABATCH, 2u * bcur) : max(acc, 1u);
         }
         if (bad_at != NO_AGENT && !s_bad) {  // block-uniform
           if (tid == 0) {
@@ -1153,6 +1161,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
           }
           __syncthreads();
         }
+      }
+      if (P.t0_delay_ticks && s_ctl.t == 0u && tid == 0) {  // diagnostic A/B: workers get a head start
+        const unsigned long long w0 = wall_clock64();
+        while (wall_clock64() - w0 < P.t0_delay_ticks) __builtin_amdgcn_s_sleep(64);
       }
       if (s_bad) {  // block-uniform: stop with the error bit set, no record for this timestep
         if (tid == 0) {
@@ -1185,6 +1197,16 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         s_hops = h;
       }
       const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
+      if (P.dbg && P.dtag && P.coop && sec == SEC_PRE1) {  // diagnostics: unresolved PRE1 pairs by agent tag
+        for (uint32_t k = tid; k < n; k += bd) {
+          const uint32_t tg = P.dtag[k] & 63u;
+          P.dtag[k] = 0u;
+          if (S.NHC[k] <= NH_STAY || S.V[k] == S.G[k] || S.GT[k] < 0) continue;
+          const uint8_t c = nh_code(P, S.GT[k], S.V[k]);
+          if (c == NH_UNKNOWN || c == NH_PENDING) atomicAdd(&P.cc->dbg_tag[0][tg], 1u);
+          else if (c == NH_PENDING_S) atomicAdd(&P.cc->dbg_tag[1][tg], 1u);
+        }
+      }
       // the pairs this step waits for go to the workers before the walk-ahead prefetch below: it
       // reads up to 8 codes per agent in dependent global loads, and publishing only after it held
       // every needed pair back ~40-60 us (round 4: the workers' enqueue -> claim delay)
@@ -1281,6 +1303,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         const int32_t tb = S.GT[b], ts = S.GT[s];
         const uint32_t candc = S.CANDC[b];
         if (vs == gs) {  // rule 3: goal swap (tswap.rs:198-202)
+          DTAG(b, 1u);
+          DTAG(s, 2u);
           uint32_t code = candc;
           if (code > NH_STAY && tb >= 0) code = nh_code(P, tb, vs);  // s's new goal is gb
           S.G[b] = gs;
@@ -1360,7 +1384,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
           // block rounds refresh + relabel below
           o.flags |= FO_ROT;
           o.ns = L;
-          for (uint32_t kk = 0; kk < L; ++kk) note_changed(ap[kk]);
+          for (uint32_t kk = 0; kk < L; ++kk) {
+            note_changed(ap[kk]);
+            DTAG(ap[kk], 4u);
+          }
           if (P.dbg) s_tick[11] += 1;  // diagnostics: rule-4 rotations
         }
         s_ctl.i = b + 1;
@@ -1525,7 +1552,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               // rule 4 on a 2-cycle k <-> s (two agents meeting head on, the common firing in 1-wide aisles):
               // the rotation (tswap.rs:241-249) is the exchange of their goals, and each one's new next hop is
               // the other's CANDC — the code of (the cell it sits on, the goal it takes)
-              const bool r2 = !r3 && onck && S.SUCC[sk] == k;
+              const bool r2 = !r3 && onck && !(P.ab_flags & 1u) && S.SUCC[sk] == k;
               bool ok = (r3 && vk != p_gs) || r2;  // rule 3 without a shared start cell, or the 2-cycle
               if (ok && code > NH_STAY) code = p_tk >= 0 ? nh_code(P, p_tk, p_vs) : NH_UNKNOWN;
               ok = ok && code <= NH_STAY;
@@ -1632,6 +1659,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                 const uint64_t batch = cut >= 64u ? m : (m & ((1ull << cut) - 1ull));
                 const bool inb = ((batch >> lane) & 1ull) != 0ull;
                 if (inb) {  // rule 3 (tswap.rs:198-202): b <-> s goals, s's new code and successor
+                  DTAG(k, 1u);
+                  DTAG(sk, 2u);
                   S.G[k] = p_gs;
                   S.GT[k] = p_ts;
                   S.G[sk] = p_gk;
@@ -1695,6 +1724,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                   S.CANDC[b] = NHC_DIRTY;
                   S.NHC[s] = (uint8_t)p_code;
                   S.SUCC[s] = p_ns;
+                  DTAG(b, r2 ? 4u : 1u);
+                  DTAG(s, r2 ? 4u : 2u);
                   if (r2) {
                     S.NHC[b] = (uint8_t)(p_code >> 8);
                     S.SUCC[b] = p_nk;
@@ -1788,6 +1819,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                         S.G[a] = ng;
                         S.GT[a] = nt;
                         S.NHC[a] = NHC_DIRTY;
+                        DTAG(a, 4u);
                       }
                       if (nc != NO_AGENT && nc + L <= LIST_CAP) {
                         if (lane < L) list[nc + lane] = a;
@@ -1941,9 +1973,19 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       }
       if (s_abort) continue;  // watchdog: exit at the top of the section loop, position kept
       if (s_exit) break;
+      // agents the phase changed since the last relabel (fast rule-3 swaps and 2-cycle rotations never
+      // take the relabel path): their new paths walked ahead and their rules candidates queued now, as
+      // the relabel path does — the movement phase and the next step read them
+      if (P.prefetch && s_cnt != 0u && !(P.ab_flags & 2u)) {
+        if (P.wide_prefetch && s_cnt != NO_AGENT) rules_prefetch_list(P, S, s_q, list, s_cnt);
+        else rules_prefetch(P, S, s_q);
+        if (P.coop && tid == 0) coop_publish(P, s_q);
+        __syncthreads();
+      }
       if (tid == 0) {
         s_ctl.section = SEC_PRE2;
         s_ctl.i = 0;
+        s_cnt = 0;
       }
       __syncthreads();
     } else if (sec == SEC_MOVE && P.has_dups) {
@@ -2059,6 +2101,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         S.DEC[k] = DEC_DONE;
         if (d == DEC_STAY) return;
         const uint32_t u = S.SUCC[k], v = S.V[k];
+        DTAG(k, 8u);
         if (d == DEC_MOVE) {
           S.V[k] = u;
           S.OCC[u] = k;
@@ -2066,6 +2109,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
           S.NHC[k] = NHC_DIRTY;
         } else {
           const uint32_t j = S.OCC[u] & OCC_IDX;
+          DTAG(j, 8u);
           S.V[k] = u;
           S.V[j] = v;
           S.OCC[u] = k;
