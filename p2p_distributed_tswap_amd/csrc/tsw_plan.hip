@@ -556,6 +556,16 @@ __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint3
 
 __device__ __forceinline__ void prefetch_changed(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t k) {
   if (spec_full(P, s_q)) return;
+  // heading to a pickup: its new goal is where the state machine switches it to the delivery
+  // (tswap.rs:113-118) — the (goal cell, delivery) pair, a step before nextnext_prefetch would queue it
+  if (P.mode != MODE_STEP && P.m > 0 && P.st[k] == ST_TO_PICKUP) {
+    const int32_t tk = P.task[k];
+    if (tk >= 0 && (uint32_t)tk < P.m) {
+      const uint32_t pc = S.G[k], dc = P.dlv[tk];
+      const int32_t dt = dc == CELL_BAD ? -1 : P.goal_tab[dc];
+      if (dt >= 0 && pc != dc && P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) prefetch_pair(P, pc, dc, dt, s_q);
+    }
+  }
   const int32_t tab = S.GT[k];
   if (tab < 0) return;
   const uint8_t c = S.NHC[k];
