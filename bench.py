@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-bfs", action="store_true", help="skip the K1 BFS measurement")
     ap.add_argument("--no-plan", action="store_true", help="skip the planning leg (profiling K1 alone)")
+    ap.add_argument("--no-sharded", action="store_true", help=argparse.SUPPRESS)  # round-4 scripts: now the default
     ap.add_argument("--sharded-k3", action="store_true",
                     help="N > 1: also run the sharded-K3 C5 leg (per-step query batches by goal owner); a measured "
                          "null result, off by default (DESIGN.md, Multi-GPU)")

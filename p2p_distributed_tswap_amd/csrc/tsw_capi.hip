@@ -68,6 +68,9 @@ struct Tunables {
   uint32_t wave_rules_max = 0xFFFFFFFFu;  // TSW_WAVE_RULES_MAX: wave-0 rules rounds when n <= this
   uint32_t wide_prefetch = 8;     // TSW_WIDE_PREFETCH: resolved hops walked ahead (0 = candidates only)
   uint32_t wide_hi = 16, wide_lo = 4;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops with a small / large speculative backlog
+  bool hot_chains = true;         // TSW_HOT_CHAINS=0: no planner-fed chains of just-assigned tasks (A/B)
+  uint32_t chain_hops = 0;        // TSW_CHAIN_HOPS: hops resolved per task chain (0: the whole path)
+  uint32_t urgent_hops = 1;       // TSW_URGENT_HOPS: walk-ahead pairs this close are queued as needed (0: off)
   uint32_t dag_width = 4;         // TSW_DAG_WIDTH: cells per DAG prefetch level (<= 16)
   uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
   uint32_t prefetch_ext = 7;      // TSW_PREFETCH_EXT: bit 0 DAG from an agent's own unresolved cell, bit 1 walk past the pickup, bit 2 walk-ahead for agents a firing changed (C3 476 -> 409 ms with bits 0-1)
@@ -125,6 +128,9 @@ struct Tunables {
     t.wide_lo = (uint32_t)num("TSW_WIDE_LO", 1, 1 << 16, t.wide_lo);
     t.dag_prefetch = (uint32_t)num("TSW_DAG_PREFETCH", 0, 16, t.dag_prefetch);
     t.dag_width = (uint32_t)num("TSW_DAG_WIDTH", 1, 16, t.dag_width);
+    t.urgent_hops = (uint32_t)num("TSW_URGENT_HOPS", 0, 16, t.urgent_hops);
+    t.chain_hops = (uint32_t)num("TSW_CHAIN_HOPS", 0, 1000000, t.chain_hops);
+    t.hot_chains = num("TSW_HOT_CHAINS", 0, 1, t.hot_chains ? 1 : 0) != 0;
     t.ab_flags = (uint32_t)num("TSW_AB_FLAGS", 0, 255, t.ab_flags);
     t.t0_delay_us = (uint32_t)num("TSW_T0_DELAY_US", 0, 10000000, t.t0_delay_us);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
@@ -237,6 +243,8 @@ struct tsw_ctx {
   AstarQuery* d_QS = nullptr;
   size_t qscap = 0;
   AstarQuery* d_QT = nullptr;    // task chains of the current plan (host-filled)
+  AstarQuery* d_QH = nullptr;    // hot task chains (planner-filled at assignment), one slot per task
+  size_t qhcap = 0;
   size_t qtcap = 0;
   uint32_t qt_count = 0;
   uint32_t* h_flags = nullptr;   // pinned, coherent: [0] planner resident, [1] abort, [2] heartbeat
@@ -1197,7 +1205,9 @@ int ensure_agents(tsw_ctx* c, size_t n) {
 // the second stream and the host-visible "planner resident" flag.
 int ensure_coop(tsw_ctx* c, uint32_t n, uint32_t max_t = 0) {
   TRY(ensure_astar_scratch(c));
-  TRY(ensure_queue(c, std::max<size_t>(4 * (size_t)n + 4096, (size_t)1 << 18)));
+  // the needed queue is linear over a coop launch too (urgent walk-ahead pairs join it): sized by the plan
+  TRY(ensure_queue(c, std::max<size_t>(std::max<size_t>(4 * (size_t)n + 4096, (size_t)1 << 18),
+                                       std::min<size_t>((size_t)n * (max_t + 1u) / 8u, (size_t)1 << 25))));
   if (!c->d_cc) {
     HIPCHK(hipMalloc(&c->d_cc, sizeof(CoopCtl)));
     HIPCHK(hipHostMalloc(&c->h_cc, sizeof(CoopCtl), hipHostMallocDefault));
@@ -1253,6 +1263,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.spec_hi = 0;  // set per launch from the worker count (run_plan_impl)
   P.dag_prefetch = c->tun.dag_prefetch;
   P.dag_width = c->tun.dag_width;
+  P.urgent_hops = c->tun.urgent_hops;
   P.ab_flags = c->tun.ab_flags;
   P.t0_delay_ticks = c->tun.t0_delay_us * 100u;
   P.prefetch_ext = c->tun.prefetch_ext;
@@ -1321,6 +1332,8 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
     P.QS = c->d_QS;
     P.qscap = (uint32_t)c->qscap;
     P.cc = c->d_cc;
+    P.QH = (mode == MODE_MAPD && c->tun.task_chains && c->tun.hot_chains && c->d_QH && m) ? c->d_QH : nullptr;
+    P.qhcap = P.QH ? (uint32_t)std::min<size_t>(c->qhcap, m) : 0u;
   }
   return P;
 }
@@ -1383,6 +1396,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.QN = c->d_Q;
     W.QS = c->d_QS;
     W.QT = c->d_QT;
+    W.QH = c->d_QH;
     W.nh = c->d_nh;
     W.nstride = c->tstride;
     // every worker may walk task chains: a chain worker serves queued needed / speculative pairs
@@ -1391,6 +1405,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     // (it was a quarter with many agents, a half otherwise)
     W.tmask = c->tun.chain_mask >= 0 ? (uint32_t)c->tun.chain_mask : 0u;
     W.preempt = c->tun.chain_preempt ? 1u : 0u;
+    W.chain_hops = c->tun.chain_hops;
     W.avoid_xcc = c->tun.avoid_xcc ? 1u : 0u;
     W.hflags = c->d_flags;
     const WorkerCfg wcfg =
@@ -1715,6 +1730,10 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
         HIPCHK(hipStreamSynchronize(c->s));
       }
       c->qt_count = (uint32_t)qt.size();
+      if (c->tun.hot_chains && (m > c->qhcap || !c->d_QH)) {
+        HIPCHK(hipStreamSynchronize(c->s));
+        HIPCHK(dgrow(c->d_QH, c->qhcap, (size_t)m));
+      }
     }
   }
   PlanArgs P = plan_args(c, n, m, MODE_MAPD, goal_out != nullptr);
@@ -1916,7 +1935,7 @@ void tsw_destroy(tsw_ctx* c) {
   if (c->h_dups) (void)hipHostFree(c->h_dups);
   fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_dtag); fre(c->d_live); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
-  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
+  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_QH); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->h_stat) hipHostFree(c->h_stat);

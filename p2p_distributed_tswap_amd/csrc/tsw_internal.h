@@ -71,6 +71,8 @@ struct CoopCtl {
   uint32_t claim_s, pad3[31];  // speculative queue: claimed
   uint32_t head_t, pad5[31];   // task-chain queue (filled by the host before the launch)
   uint32_t claim_t, pad6[31];  // task-chain queue: claimed
+  uint32_t head_h, pad9[31];   // hot task chains: tasks the planner has assigned (published like head_s)
+  uint32_t claim_h, pad10[31]; // hot task chains: claimed
   uint32_t pub, pad7[31];      // planner publish count: idle workers poll this one word
   uint32_t planner_xcc, pad8[31];  // 1 + XCD of the planner block (0: unknown), written before it signals residency
   uint32_t stop, alive, err, waits;  // planner finished / workers started / worker error bits / planner waits

@@ -56,6 +56,7 @@ struct PlanArgs {
   uint32_t spec_hi;             // coop mode: backlog (queued, unclaimed speculative pairs) counted as small up to this
   uint32_t dag_prefetch;        // walk-ahead also queues the shortest-path successors of the first unresolved cell
   uint32_t dag_width;           // ... at most this many cells per DAG level (0: 4)
+  uint32_t urgent_hops;         // coop: walk-ahead pairs within this many hops (pickup pairs within + 1) go to the needed queue
   uint32_t ab_flags;            // diagnostic A/B switches (Tunables::ab_flags; 0 in the product build)
   uint32_t t0_delay_ticks;      // diagnostic: idle after step 0's assignment (100 MHz ticks)
   uint32_t prefetch_ext;        // bit 0: DAG from an agent's own unresolved cell; bit 1: walk on past the pickup
@@ -100,6 +101,8 @@ struct PlanArgs {
   uint32_t coop;
   AstarQuery* QS;
   uint32_t qscap;
+  AstarQuery* QH;  // hot task chains: (pickup, delivery) of every task as it is assigned (qhcap = m entries)
+  uint32_t qhcap;
   CoopCtl* cc;
   // host-visible (pinned, system-coherent) words: [0] set when the planner block is resident,
   // [1] abort (host watchdog: planner waits give up, workers exit), [2] planner heartbeat (timesteps)
@@ -129,6 +132,7 @@ struct WorkerArgs {
   const AstarQuery* QN;
   const AstarQuery* QS;
   const AstarQuery* QT;  // task chains: (pickup, delivery) of every task, walked hop by hop
+  const AstarQuery* QH;  // hot task chains: the same walk for tasks the planner has just assigned (first)
   uint8_t* nh;
   uint64_t nstride;
   uint32_t hcap;      // LDS heap entries
@@ -136,6 +140,7 @@ struct WorkerArgs {
   uint32_t stage_fb;  // free-cell bitmap staged in LDS (else read from global memory / L2)
   uint32_t tmask;     // workers with (blockIdx & tmask) == tmask also take task-chain jobs
   uint32_t preempt;   // chain workers serve queued needed / speculative pairs between hops
+  uint32_t chain_hops;  // hops a chain worker resolves per task chain (0: the whole pickup -> delivery path)
   const uint32_t* hflags;  // host watchdog words (hflags[1] = abort)
   uint32_t* gs_all;   // per-wave global g-score slots (tier 2 / tier 3), ncell u32 each
   uint32_t* epochs;   // per-slot tag epochs

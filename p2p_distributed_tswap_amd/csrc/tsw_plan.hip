@@ -384,10 +384,12 @@ __device__ __forceinline__ bool plan_abort(const PlanArgs& P) {
 // (marks are only written with an entry), and the agent-scope release it would cost writes back this
 // XCD's L2. s_q[3] / s_q[4] hold the last published heads (0 = the launch's zeroed CoopCtl).
 __device__ __forceinline__ void coop_publish(const PlanArgs& P, uint32_t* s_q) {
-  const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap);
-  if (hn == s_q[3] && hs == s_q[4]) return;
+  const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap), hh = min(s_q[6], P.qhcap);
+  if (hn == s_q[3] && hs == s_q[4] && hh == s_q[7]) return;
   s_q[3] = hn;
   s_q[4] = hs;
+  s_q[7] = hh;
+  if (P.QH) __hip_atomic_store(&P.cc->head_h, hh, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&P.cc->head_s, hs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&P.cc->head_n, hn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   // wake idle workers, which poll only this word (a plain agent-scope store of a new value)
@@ -643,7 +645,10 @@ __device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, 
     if (u == g) return hops - h;
     const uint8_t cu = P.nh[(uint64_t)tab * P.nstride + u];
     if (cu == NH_UNKNOWN || cu == NH_PENDING || cu == NH_PENDING_S) {
-      if (cu == NH_UNKNOWN) prefetch_pair(P, u, g, tab, s_q);
+      // a pair the agent reads within urgent_hops steps goes to the needed queue (served before the
+      // speculative backlog, which on wh10k holds ~500 pairs when a wait starts); farther ones are speculative
+      if (P.coop && h < P.urgent_hops) enqueue_pair(P, u, g, tab, s_q);
+      else if (cu == NH_UNKNOWN) prefetch_pair(P, u, g, tab, s_q);
       if (P.dag_prefetch) dag_prefetch(P, s_q, u, g, tab);
       return 0;
     }
@@ -678,7 +683,13 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
         const int32_t dt = dc == CELL_BAD ? -1 : P.goal_tab[dc];
         if (dt >= 0 && pc != dc) {
           dtab = dt;
-          if (P.nh[(uint64_t)dt * P.nstride + pc] == NH_UNKNOWN) prefetch_pair(P, pc, dc, dt, s_q);
+          const uint8_t cp = P.nh[(uint64_t)dt * P.nstride + pc];
+          const uint32_t vk = S.V[k], W = P.W;
+          const uint32_t vx = vk % W, vy = vk / W, px = pc % W, py = pc / W;
+          const uint32_t man = (vx > px ? vx - px : px - vx) + (vy > py ? vy - py : py - vy);
+          // arriving within urgent_hops + 1 steps (Manhattan bounds the path from below): needed queue
+          if (P.coop && man <= P.urgent_hops + 1u && (cp == NH_UNKNOWN || cp == NH_PENDING_S)) enqueue_pair(P, pc, dc, dt, s_q);
+          else if (cp == NH_UNKNOWN) prefetch_pair(P, pc, dc, dt, s_q);
         }
       }
     }
@@ -778,7 +789,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     return;
   }
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[6], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort, s_hops,
+  __shared__ uint32_t s_q[8], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort, s_hops,
       s_badat;
   __shared__ uint32_t s_ap[128];  // rules: members of a rule-4 cycle rotated by the wave (<= 64), links
   __shared__ uint32_t s_wcount[16];
@@ -902,6 +913,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     s_q[3] = 0;  // last published needed / speculative heads (coop mode)
     s_q[4] = 0;
     s_q[5] = s_ctl.t;  // the timestep speculative entries are queued in (coop mode)
+    s_q[6] = 0;  // hot task chains queued this launch (coop mode)
+    s_q[7] = 0;  // ... last published head
     if (P.coop) __hip_atomic_store(&P.cc->t_now, s_ctl.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int k = 0; k < 40; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
@@ -1156,6 +1169,28 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               S.G[ai] = ng;
               S.GT[ai] = P.goal_tab[ng];
               S.NHC[ai] = NHC_DIRTY;
+              // the task's pickup -> delivery path goes to the workers now (hot chain), ahead of the
+              // index-ordered walk of every task's chain: this one is about to be carried
+              const uint32_t dc = P.dlv[t];
+              if (P.QH && dc != CELL_BAD && dc != ng) {
+                const int32_t dtab = P.goal_tab[dc];
+                const uint32_t qi = atomicAdd(&s_q[6], 1u);
+                if (dtab >= 0 && qi < P.qhcap) {
+                  AstarQuery q;
+                  q.v = ng;
+                  q.goal = dc;
+                  q.tab = dtab;
+                  q.out = 0u;
+                  P.QH[qi] = q;
+                } else if (dtab < 0 && qi < P.qhcap) {
+                  AstarQuery q;  // keep the slot well-formed: a chain without a table is skipped
+                  q.v = ng;
+                  q.goal = dc;
+                  q.tab = -1;
+                  q.out = 0u;
+                  P.QH[qi] = q;
+                }
+              }
             }
           }
           __syncthreads();

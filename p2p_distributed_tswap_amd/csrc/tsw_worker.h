@@ -79,6 +79,15 @@ __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool tak
         continue;
       }
       if (take_t) {
+        // hot chains first: tasks the planner has just assigned
+        const uint32_t hh = w_ld(&cc->head_h), ch = w_ld(&cc->claim_h);
+        if (ch < hh) {
+          if (w_cas(&cc->claim_h, ch, ch + 1u)) {
+            *idx = ch;
+            return 3;
+          }
+          continue;
+        }
         const uint32_t ht = w_ld(&cc->head_t), ct = w_ld(&cc->claim_t);
         if (ct < ht) {
           if (w_cas(&cc->claim_t, ct, ct + 1u)) {
@@ -355,7 +364,9 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
     // the entry was published by the planner's release of the head (or by the host before the
     // launch): read it past stale caches
-    const uint32_t* e = reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : A.QT) + idx);
+    const uint32_t* e =
+        reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : which == 3 ? A.QH : A.QT) + idx);
+    if (which == 3) which = 2;  // a hot chain is walked as any task chain
     const uint32_t v = w_ld(e), goal = w_ld(e + 1);
     const int32_t tab = (int32_t)w_ld(e + 2);
     cur_q = (uint32_t)which;
@@ -382,7 +393,8 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     // or at the goal. Pairs are not marked pending, so an abandoned chain leaves nothing behind.
     if (tab < 0) continue;
     uint32_t c = v;
-    for (uint32_t hop = 0; hop < ncell && c != goal; ++hop) {
+    const uint32_t max_hops = A.chain_hops ? A.chain_hops : ncell;
+    for (uint32_t hop = 0; hop < max_hops && c != goal; ++hop) {
       // the planner is done: abandon the rest of the chain (nothing is marked pending)
       if ((uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? w_ld(&A.cc->stop) : 0u)) break;
       // pairs the planner queued meanwhile come first (A.preempt)
