@@ -70,6 +70,7 @@ struct Tunables {
   uint32_t wide_hi = 16, wide_lo = 4;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops with a small / large speculative backlog
   bool hot_chains = true;         // TSW_HOT_CHAINS=0: no planner-fed chains of just-assigned tasks (A/B)
   uint32_t chain_hops = 0;        // TSW_CHAIN_HOPS: hops resolved per task chain (0: the whole path)
+  uint32_t predict = 1;           // TSW_PREDICT: predicted task chains, bit 0 at pickups, bit 1 at delivery-goal changes (0: off)
   uint32_t urgent_hops = 1;       // TSW_URGENT_HOPS: walk-ahead pairs this close are queued as needed (0: off)
   uint32_t dag_width = 4;         // TSW_DAG_WIDTH: cells per DAG prefetch level (<= 16)
   uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
@@ -131,6 +132,7 @@ struct Tunables {
     t.urgent_hops = (uint32_t)num("TSW_URGENT_HOPS", 0, 16, t.urgent_hops);
     t.chain_hops = (uint32_t)num("TSW_CHAIN_HOPS", 0, 1000000, t.chain_hops);
     t.hot_chains = num("TSW_HOT_CHAINS", 0, 1, t.hot_chains ? 1 : 0) != 0;
+    t.predict = (uint32_t)num("TSW_PREDICT", 0, 3, t.predict);
     t.ab_flags = (uint32_t)num("TSW_AB_FLAGS", 0, 255, t.ab_flags);
     t.t0_delay_us = (uint32_t)num("TSW_T0_DELAY_US", 0, 10000000, t.t0_delay_us);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
@@ -245,6 +247,10 @@ struct tsw_ctx {
   AstarQuery* d_QT = nullptr;    // task chains of the current plan (host-filled)
   AstarQuery* d_QH = nullptr;    // hot task chains (planner-filled at assignment), one slot per task
   size_t qhcap = 0;
+  uint2* d_QP = nullptr;         // predicted task chains (planner-filled at pickups), PlanArgs::QP
+  size_t qpcap = 0;
+  uint32_t* d_pred = nullptr;    // TSW_PLAN_DEBUG: per-agent last predicted task
+  size_t predcap = 0;
   size_t qtcap = 0;
   uint32_t qt_count = 0;
   uint32_t* h_flags = nullptr;   // pinned, coherent: [0] planner resident, [1] abort, [2] heartbeat
@@ -284,6 +290,11 @@ struct tsw_ctx {
   // tasks
   size_t tcap = 0;
   uint32_t *d_live = nullptr, *d_pick = nullptr, *d_dlv = nullptr, *d_unused = nullptr;
+  // K4 spatial index (PlanArgs::klt / kpos / kbox / kcnt), rebuilt by every plan call
+  uint32_t *d_klt = nullptr, *d_kpos = nullptr, *d_kcnt = nullptr;
+  uint2* d_kbox = nullptr;
+  size_t kcap = 0, kchcap = 0;
+  uint32_t kchunks = 0;
   // records
   uint64_t* d_rec = nullptr;
   size_t rec_cap = 0;
@@ -1270,16 +1281,11 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.dist = c->d_dist;
   P.nbmask = c->d_nbmask;
   P.live = c->d_live;
-  {
-    // K4 32-bit keys: task ids need kshift bits with 2^kshift > m (a valid key is never 0xFFFFFFFF, the
-    // taken marker); distances saturate at DSAT = 2^(32 - kshift) - 1. Exact when DSAT exceeds every
-    // on-grid distance (W + H - 2): a key at DSAT then belongs to an off-grid pickup, and if the minimum
-    // is saturated every task left is off-grid — assigning any of them fails as the reference panics.
-    uint32_t kb = 1;
-    while (kb < 31u && (1ull << kb) <= (uint64_t)m) ++kb;
-    P.kshift = kb;
-    P.key32 = ((1ull << (32u - kb)) - 1ull) > (uint64_t)c->G.W + c->G.H ? 1u : 0u;
-  }
+  P.klt = c->d_klt;
+  P.kpos = c->d_kpos;
+  P.kbox = c->d_kbox;
+  P.kcnt = c->d_kcnt;
+  P.kchunks = c->kchunks;
   P.pick = c->d_pick;
   P.dlv = c->d_dlv;
   P.goal_tab = c->d_goal_tab;
@@ -1302,6 +1308,16 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
     }
     if (c->d_dtag && hipMemsetAsync(c->d_dtag, 0, (size_t)n * 4, c->s) == hipSuccess) P.dtag = c->d_dtag;
   }
+  P.pred = nullptr;
+  if (P.dbg && n && mode == MODE_MAPD) {  // diagnostics only: prediction hits
+    if (c->predcap < n) {
+      if (c->d_pred) (void)hipFree(c->d_pred);
+      c->d_pred = nullptr;
+      c->predcap = 0;
+      if (hipMalloc(&c->d_pred, (size_t)n * 4) == hipSuccess) c->predcap = n;
+    }
+    if (c->d_pred && hipMemsetAsync(c->d_pred, 0xFF, (size_t)n * 4, c->s) == hipSuccess) P.pred = c->d_pred;
+  }
   // LDS residency, in priority order: agents, occupancy grid, task table
   const size_t budget = (size_t)std::max(c->max_lds - 2048, 0);
   bool ag = plan_lds_bytes(n, P.ncell, m, true, false, false) <= budget;
@@ -1318,7 +1334,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   // OCC: C3's 170x84 fits OCC but not MU beside the agent arrays)
   bool mu = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, true, part) <= budget;
   bool oc = mu || (c->tun.occ_split && plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, false, part) <= budget);
-  bool tk = m > 0 && plan_lds_bytes(n, P.ncell, m, ag, oc, true, fl, mu, part) <= budget;
+  const bool tk = false;  // K4 reads its spatial index from global memory (the chunks it needs only)
   P.part_lds = part;
   P.f_lds = fl;
   P.mu_lds = mu;
@@ -1334,7 +1350,11 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
     P.cc = c->d_cc;
     P.QH = (mode == MODE_MAPD && c->tun.task_chains && c->tun.hot_chains && c->d_QH && m) ? c->d_QH : nullptr;
     P.qhcap = P.QH ? (uint32_t)std::min<size_t>(c->qhcap, m) : 0u;
+    P.QP = (P.QH && c->tun.predict && c->d_QP) ? c->d_QP : nullptr;
+    P.qpcap = P.QP ? (uint32_t)std::min<size_t>(c->qpcap, 0xFFFFFFFFu) : 0u;
+    P.predict = P.QP ? c->tun.predict : 0u;
   }
+  if (!P.QP) P.pred = nullptr;
   return P;
 }
 
@@ -1397,6 +1417,16 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.QS = c->d_QS;
     W.QT = c->d_QT;
     W.QH = c->d_QH;
+    W.QP = P.QP;
+    W.klive = c->d_live;
+    W.klt = c->d_klt;
+    W.kbox = c->d_kbox;
+    W.kcnt = c->d_kcnt;
+    W.kchunks = c->kchunks;
+    W.pick = c->d_pick;
+    W.dlv = c->d_dlv;
+    W.goal_tab = c->d_goal_tab;
+    W.pred = P.pred;
     W.nh = c->d_nh;
     W.nstride = c->tstride;
     // every worker may walk task chains: a chain worker serves queued needed / speculative pairs
@@ -1582,6 +1612,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
           }
           fprintf(stderr, "[k_plan] speculative pairs dropped as stale: %u (older than %u timesteps)\n",
                   cc.spec_dropped, c->tun.stale_steps);
+          fprintf(stderr, "[k_plan] predicted chains: %u jobs | assignments %u: predicted task %u, no prediction %u\n",
+                  cc.pred_jobs, cc.pred_asg, cc.pred_hit, cc.pred_none);
           fprintf(stderr, "[k_plan] spec backlog at wait start: avg %.1f max %u | queue delay enqueue -> claim: needed "
                   "avg %.1f us (%u > 1 ms, %u already resolved), speculative avg %.1f timesteps (%u > 1, %u already resolved)\n",
                   cc.waits ? (double)cc.dbg_depth / cc.waits : 0.0, cc.dbg_depth_max,
@@ -1643,8 +1675,13 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   if (!out_T || (n && (!starts || !out)) || (m && !tasks)) RET(TSW_EINVAL, "null argument");
   if (max_t > (1u << 20)) RET(TSW_EINVAL, "max_t too large");
   TRY(set_device(c));
-  const uint32_t m4 = (m + 3u) & ~3u;  // K4 reads the live array as 16-B vectors
-  std::vector<uint32_t> vcell(n), pick(m), dlv(m), live(std::max<uint32_t>(m4, 4u), TASK_TAKEN);
+  // K4 spatial index: tasks in Morton order of their (clamped) pickup points, cut into chunks of KCH = 32
+  // entries with static bounding boxes (tsw_plan.h PlanArgs::kbox)
+  constexpr uint32_t KCHH = 32;
+  const uint32_t nch = std::max<uint32_t>((m + KCHH - 1u) / KCHH, 1u);
+  std::vector<uint32_t> vcell(n), pick(m), dlv(m), pxy(m), live((size_t)nch * KCHH, TASK_TAKEN),
+      klt((size_t)nch * KCHH, 0xFFFFFFFFu), kpos(std::max<uint32_t>(m, 1u)), kcnt(nch, 0u);
+  std::vector<uint2> kbox(nch, make_uint2(0u, 0u));
   std::vector<uint32_t> goalset;
   goalset.reserve(n + 2 * (size_t)m);
   for (uint32_t i = 0; i < n; ++i) {
@@ -1662,9 +1699,35 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   for (uint32_t k = 0; k < m; ++k) {
     if (!cell_ok(c, tasks[k].pickup.x, tasks[k].pickup.y, &pick[k])) pick[k] = CELL_BAD;
     if (!cell_ok(c, tasks[k].delivery.x, tasks[k].delivery.y, &dlv[k])) dlv[k] = CELL_BAD;
-    live[k] = std::min<uint32_t>(tasks[k].pickup.x, 0xFFFEu) | (std::min<uint32_t>(tasks[k].pickup.y, 0xFFFEu) << 16);
+    pxy[k] = std::min<uint32_t>(tasks[k].pickup.x, 0xFFFEu) | (std::min<uint32_t>(tasks[k].pickup.y, 0xFFFEu) << 16);
     if (pick[k] != CELL_BAD) goalset.push_back(pick[k]);
     if (dlv[k] != CELL_BAD) goalset.push_back(dlv[k]);
+  }
+  {
+    auto morton = [](uint32_t xy) {
+      uint64_t z = 0;
+      for (uint32_t bt = 0; bt < 16u; ++bt)
+        z |= (uint64_t)((xy >> bt) & 1u) << (2u * bt) | (uint64_t)((xy >> (16u + bt)) & 1u) << (2u * bt + 1u);
+      return z;
+    };
+    std::vector<std::pair<uint64_t, uint32_t>> ord(m);
+    for (uint32_t k = 0; k < m; ++k) ord[k] = {morton(pxy[k]), k};
+    std::sort(ord.begin(), ord.end());
+    for (uint32_t pos = 0; pos < m; ++pos) {
+      const uint32_t k = ord[pos].second, xy = pxy[k], ch = pos / KCHH;
+      live[pos] = xy;
+      klt[pos] = k;
+      kpos[k] = pos;
+      const uint32_t x = xy & 0xFFFFu, y = xy >> 16;
+      uint2& bx = kbox[ch];
+      if (kcnt[ch] == 0u) {
+        bx = make_uint2(xy, xy);
+      } else {
+        bx.x = std::min(bx.x & 0xFFFFu, x) | (std::min(bx.x >> 16, y) << 16);
+        bx.y = std::max(bx.y & 0xFFFFu, x) | (std::max(bx.y >> 16, y) << 16);
+      }
+      ++kcnt[ch];
+    }
   }
   TRY(ensure_agents(c, std::max<uint32_t>(n, 1)));
   if (live.size() > c->tcap || !c->d_live) {
@@ -1676,6 +1739,21 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
     c->tcap = std::min(std::min(a, b), d);
     if (!c->d_unused) HIPCHK(hipMalloc(&c->d_unused, 4));
   }
+  if (live.size() > c->kcap || !c->d_klt) {
+    HIPCHK(hipStreamSynchronize(c->s));
+    size_t a = c->kcap, b = c->kcap;
+    HIPCHK(dgrow(c->d_klt, a, live.size()));
+    HIPCHK(dgrow(c->d_kpos, b, live.size()));
+    c->kcap = std::min(a, b);
+  }
+  if (nch > c->kchcap || !c->d_kbox) {
+    HIPCHK(hipStreamSynchronize(c->s));
+    size_t a = c->kchcap, b = c->kchcap;
+    HIPCHK(dgrow(c->d_kbox, a, (size_t)nch));
+    HIPCHK(dgrow(c->d_kcnt, b, (size_t)nch));
+    c->kchcap = std::min(a, b);
+  }
+  c->kchunks = nch;
   const size_t stride_t = (size_t)max_t + 1;
   const size_t recs = stride_t * std::max<uint32_t>(n, 1);
   if (recs > c->rec_cap || !c->d_rec) {
@@ -1694,6 +1772,10 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
     HIPCHK(hipMemsetAsync(c->d_task, 0xFF, n * 4ull, c->s));
   }
   HIPCHK(hipMemcpyAsync(c->d_live, live.data(), live.size() * 4ull, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_klt, klt.data(), klt.size() * 4ull, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_kpos, kpos.data(), kpos.size() * 4ull, hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_kbox, kbox.data(), kbox.size() * sizeof(uint2), hipMemcpyHostToDevice, c->s));
+  HIPCHK(hipMemcpyAsync(c->d_kcnt, kcnt.data(), kcnt.size() * 4ull, hipMemcpyHostToDevice, c->s));
   if (m) {
     HIPCHK(hipMemcpyAsync(c->d_pick, pick.data(), m * 4ull, hipMemcpyHostToDevice, c->s));
     HIPCHK(hipMemcpyAsync(c->d_dlv, dlv.data(), m * 4ull, hipMemcpyHostToDevice, c->s));
@@ -1733,6 +1815,13 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
       if (c->tun.hot_chains && (m > c->qhcap || !c->d_QH)) {
         HIPCHK(hipStreamSynchronize(c->s));
         HIPCHK(dgrow(c->d_QH, c->qhcap, (size_t)m));
+      }
+      // predictions: one per pickup (<= m) plus, with bit 1, one per goal change of a delivering agent;
+      // a full queue only stops predicting
+      const size_t qp = (size_t)m + 16u * (size_t)n * (c->tun.predict & 2u ? 8u : 0u);
+      if (c->tun.hot_chains && c->tun.predict && (qp > c->qpcap || !c->d_QP)) {
+        HIPCHK(hipStreamSynchronize(c->s));
+        HIPCHK(dgrow(c->d_QP, c->qpcap, qp));
       }
     }
   }
@@ -1933,9 +2022,9 @@ void tsw_destroy(tsw_ctx* c) {
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
   fre(c->d_gt); fre(c->d_dec); fre(c->d_mu); fre(c->d_dups); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
   if (c->h_dups) (void)hipHostFree(c->h_dups);
-  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_dtag); fre(c->d_live); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
+  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_dtag); fre(c->d_live); fre(c->d_klt); fre(c->d_kpos); fre(c->d_kbox); fre(c->d_kcnt); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
-  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_QH); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
+  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_QH); fre(c->d_QP); fre(c->d_pred); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->h_stat) hipHostFree(c->h_stat);

@@ -73,6 +73,8 @@ struct CoopCtl {
   uint32_t claim_t, pad6[31];  // task-chain queue: claimed
   uint32_t head_h, pad9[31];   // hot task chains: tasks the planner has assigned (published like head_s)
   uint32_t claim_h, pad10[31]; // hot task chains: claimed
+  uint32_t head_p, pad11[31];   // predicted task chains: delivery cells whose next task a worker predicts
+  uint32_t claim_p, pad12[31];  // predicted task chains: claimed
   uint32_t pub, pad7[31];      // planner publish count: idle workers poll this one word
   uint32_t planner_xcc, pad8[31];  // 1 + XCD of the planner block (0: unknown), written before it signals residency
   uint32_t stop, alive, err, waits;  // planner finished / workers started / worker error bits / planner waits
@@ -104,6 +106,8 @@ struct CoopCtl {
   // what changed them since the previous PRE1 (PlanArgs::dtag bits: 1 rule-3 b, 2 rule-3 s, 4 rotated,
   // 8 moved, 16 assigned, 32 picked up), [0] unknown / [1] pending-speculative per tag combination
   uint32_t dbg_tag[2][64];
+  // predicted task chains: jobs run, and (TSW_PLAN_DEBUG) assignments whose task was the agent's last prediction
+  uint32_t pred_jobs, pred_asg, pred_hit, pred_none;
 };
 
 struct AstarQuery {

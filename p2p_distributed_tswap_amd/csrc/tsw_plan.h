@@ -77,12 +77,16 @@ struct PlanArgs {
   uint32_t* mk;   // per agent batch marks of the wave rules rounds (global copy, n + 1 entries)
   uint32_t* occ;  // per cell occupancy
   uint64_t* mu;   // per cell round-tagged lowest undecided targeting agent (global copy)
-  // K4: per task its pickup point (x | y << 16, coordinates clamped to 0xFFFE) while unused, TASK_TAKEN
-  // once assigned; padded with TASK_TAKEN to a multiple of 4 entries (the scan reads 16-B vectors)
+  // K4 spatial index (tsw_capi.hip plan_impl): the tasks in Morton order of their pickup points (coordinates
+  // clamped to 0xFFFE). live[pos] = pickup point (x | y << 16) while unused, TASK_TAKEN once assigned; klt[pos] =
+  // the task index; kpos[task] = its position; chunks of KCH positions have a static bounding box kbox
+  // (x0 | y0 << 16, x1 | y1 << 16) and a count of untaken entries kcnt. Padding entries are TASK_TAKEN.
   uint32_t* live;
-  // K4 keys: (min(distance, 2^(32 - kshift) - 1) << kshift) | task as one u32 when key32 (2^kshift > m and
-  // the saturation level exceeds every on-grid distance; tsw_capi.hip plan_args), else u64, one agent at a time
-  uint32_t kshift, key32;
+  const uint32_t* klt;
+  const uint32_t* kpos;
+  const uint2* kbox;
+  uint32_t* kcnt;
+  uint32_t kchunks;
   const uint32_t* pick;
   const uint32_t* dlv;
   const int32_t* goal_tab;
@@ -103,6 +107,13 @@ struct PlanArgs {
   uint32_t qscap;
   AstarQuery* QH;  // hot task chains: (pickup, delivery) of every task as it is assigned (qhcap = m entries)
   uint32_t qhcap;
+  // predicted task chains: (delivery cell, agent) of an agent that picks up a task (and, with bit 1 of
+  // predict, of a delivering agent whose goal a rule changed); a worker predicts the task the agent will
+  // be assigned at that cell — the nearest untaken pickup now — and walks that task's chain (tsw_worker.h)
+  uint2* QP;
+  uint32_t qpcap;
+  uint32_t predict;     // bit 0: at pickups, bit 1: at goal changes of delivering agents
+  uint32_t* pred;       // diagnostics (TSW_PLAN_DEBUG): per agent, the task last predicted for it
   CoopCtl* cc;
   // host-visible (pinned, system-coherent) words: [0] set when the planner block is resident,
   // [1] abort (host watchdog: planner waits give up, workers exit), [2] planner heartbeat (timesteps)
@@ -133,6 +144,16 @@ struct WorkerArgs {
   const AstarQuery* QS;
   const AstarQuery* QT;  // task chains: (pickup, delivery) of every task, walked hop by hop
   const AstarQuery* QH;  // hot task chains: the same walk for tasks the planner has just assigned (first)
+  const uint2* QP;       // predicted task chains: (delivery cell, agent); the chain of the predicted task (PlanArgs::QP)
+  const uint32_t* klive;  // K4 spatial index (PlanArgs::live / klt / kbox / kcnt), read for predictions
+  const uint32_t* klt;
+  const uint2* kbox;
+  const uint32_t* kcnt;
+  uint32_t kchunks;
+  const uint32_t* pick;
+  const uint32_t* dlv;
+  const int32_t* goal_tab;
+  uint32_t* pred;         // diagnostics: per agent, the task last predicted for it (nullptr: off)
   uint8_t* nh;
   uint64_t nstride;
   uint32_t hcap;      // LDS heap entries

@@ -46,6 +46,8 @@ constexpr uint32_t SUCC_TERM = 0xFFFFFFFFu;
 constexpr uint32_t NO_AGENT = 0xFFFFFFFFu;
 constexpr uint32_t NO_CELL = 0xFFFFFFFFu;
 constexpr uint32_t ABATCH = 8;    // K4: idle agents whose nearest pickups one pass over the tasks computes
+constexpr uint32_t KCH = 32;      // K4: tasks per spatial chunk (PlanArgs::kbox / kcnt), a multiple of 16
+constexpr uint32_t KPT = 2;       // K4: chunks per thread whose count and box stay in registers across a batch
 constexpr uint32_t LIST_CAP = 1024;  // entries of the kernel's LDS `list` (ASSIGN compaction, changed agents)
 // movement-round decision states
 constexpr uint8_t DEC_OPEN = 0, DEC_DONE = 1, DEC_STAY = 2, DEC_MOVE = 3, DEC_SWAP = 4;
@@ -89,7 +91,7 @@ struct Arrays {
   uint32_t* F2;
   uint32_t* OCC;   // per cell: lowest agent | OCC_FLAG, or OCC_NONE
   uint64_t* MU;    // per cell: (round << 32) | ~(lowest undecided agent targeting it), movement rounds
-  uint32_t* LIVE;  // K4: pickup point of each unused task, TASK_TAKEN once assigned (PlanArgs::live)
+  uint32_t* LIVE;  // K4: pickup points in Morton order, TASK_TAKEN once assigned (PlanArgs::live)
   unsigned long long t0;  // wall clock at the launch (coop: "no worker has started" is measured from here)
 };
 
@@ -385,10 +387,13 @@ __device__ __forceinline__ bool plan_abort(const PlanArgs& P) {
 // XCD's L2. s_q[3] / s_q[4] hold the last published heads (0 = the launch's zeroed CoopCtl).
 __device__ __forceinline__ void coop_publish(const PlanArgs& P, uint32_t* s_q) {
   const uint32_t hn = min(s_q[0], P.qcap), hs = min(s_q[1], P.qscap), hh = min(s_q[6], P.qhcap);
-  if (hn == s_q[3] && hs == s_q[4] && hh == s_q[7]) return;
+  const uint32_t hp = min(s_q[8], P.qpcap);
+  if (hn == s_q[3] && hs == s_q[4] && hh == s_q[7] && hp == s_q[9]) return;
   s_q[3] = hn;
   s_q[4] = hs;
   s_q[7] = hh;
+  s_q[9] = hp;
+  if (P.QP) __hip_atomic_store(&P.cc->head_p, hp, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   if (P.QH) __hip_atomic_store(&P.cc->head_h, hh, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&P.cc->head_s, hs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&P.cc->head_n, hn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -556,7 +561,16 @@ __device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, 
                                   uint32_t hops);
 __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab);
 
+// coop mode: agent k will be idle at `cell` (its delivery): a worker predicts its next task and walks that
+// task's pickup -> delivery chain ahead of the assignment (s_q[8]: entries queued, PlanArgs::QP)
+__device__ __forceinline__ void predict_push(const PlanArgs& P, uint32_t* s_q, uint32_t cell, uint32_t k) {
+  const uint32_t qi = atomicAdd(&s_q[8], 1u);
+  if (qi < P.qpcap) P.QP[qi] = make_uint2(cell, k);
+}
+
 __device__ __forceinline__ void prefetch_changed(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t k) {
+  // delivering: a rule handed the agent another delivery cell, so its next task changes with it
+  if ((P.predict & 2u) && P.QP && P.st[k] == ST_TO_DELIVERY) predict_push(P, s_q, S.G[k], k);
   if (spec_full(P, s_q)) return;
   // heading to a pickup: its new goal is where the state machine switches it to the delivery
   // (tswap.rs:113-118) — the (goal cell, delivery) pair, a step before nextnext_prefetch would queue it
@@ -789,13 +803,13 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     return;
   }
   __shared__ PlanCtl s_ctl;
-  __shared__ uint32_t s_q[8], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort, s_hops,
+  __shared__ uint32_t s_q[10], s_need, s_cnt, s_doit, s_px, s_py, s_exit, s_best, s_miss, s_flag, s_abort, s_cabort, s_hops,
       s_badat;
   __shared__ uint32_t s_ap[128];  // rules: members of a rule-4 cycle rotated by the wave (<= 64), links
   __shared__ uint32_t s_wcount[16];
   __shared__ uint64_t s_red[16];
   __shared__ uint64_t s_bestk[ABATCH];  // K4: per batch agent, block minimum of (distance, task) (LDS atomic min)
-  __shared__ uint32_t s_apos[ABATCH], s_acct[ABATCH], s_cnt2, s_bestk32[ABATCH];
+  __shared__ uint32_t s_apos[ABATCH], s_acct[ABATCH], s_cnt2, s_ub[ABATCH];
   __shared__ unsigned long long s_tick[40], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
   __shared__ uint32_t s_bad;               // ASSIGN looked up an off-grid/blocked task cell
@@ -877,12 +891,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     S.OCC = P.occ;
     S.MU = P.mu;
   }
-  if (P.tasks_lds) {
-    S.LIVE = reinterpret_cast<uint32_t*>(carve((size_t)((P.m + 3u) & ~3u) * 4));
-    for (uint32_t k = tid; k < ((P.m + 3u) & ~3u); k += bd) S.LIVE[k] = P.live[k];
-  } else {
-    S.LIVE = P.live;
-  }
+  S.LIVE = P.live;
   for (uint32_t k = tid; k <= n; k += bd) S.MK[k] = 0xFFFFFFFFu;
   for (uint32_t k = tid; k < n; k += bd) {
     const uint32_t g = P.g[k];
@@ -915,6 +924,8 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
     s_q[5] = s_ctl.t;  // the timestep speculative entries are queued in (coop mode)
     s_q[6] = 0;  // hot task chains queued this launch (coop mode)
     s_q[7] = 0;  // ... last published head
+    s_q[8] = 0;  // predicted task chains queued this launch (coop mode)
+    s_q[9] = 0;  // ... last published head
     if (P.coop) __hip_atomic_store(&P.cc->t_now, s_ctl.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int k = 0; k < 40; ++k) s_tick[k] = 0;
     s_tlast = wall_clock64();
@@ -989,7 +1000,6 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         }
       }
       __syncthreads();
-      const uint32_t m4 = (P.m + 3u) & ~3u;
       for (uint32_t base = 0; base < n && !s_bad; base += bd) {
         const uint32_t i = base + tid;
         bool idle = false;
@@ -1012,6 +1022,7 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
                   S.G[i] = ng;
                   S.GT[i] = P.goal_tab[ng];
                   S.NHC[i] = NHC_DIRTY;
+                  if ((P.predict & 1u) && P.QP) predict_push(P, s_q, ng, i);
                 }
               }
             } else {  // ST_TO_DELIVERY
@@ -1055,82 +1066,120 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
             const uint32_t v = S.V[list[kk + tid]];
             s_apos[tid] = (v % W) | ((v / W) << 16);
             s_bestk[tid] = ~0ull;
-            s_bestk32[tid] = 0xFFFFFFFFu;
+            s_ub[tid] = 0xFFFFFFFFu;
           }
           __syncthreads();
-          // One 32-bit key per batch agent and thread: (min(distance, DSAT) << kshift) | task — comparable
-          // across threads, reduced with the DPP wave min; the batch agents' cells sit in SGPRs
-          // (block-uniform). A taken task's key is all ones and never wins. Without 32-bit keys
-          // (P.key32 == 0: huge task sets or grids) one agent per batch with 64-bit keys.
-          const uint32_t q4 = m4 >> 2;
-          const bool k32 = P.key32 != 0u;
-          const uint32_t ksh = P.kshift, dsat = (uint32_t)((1ull << (32u - ksh)) - 1ull);
-          uint32_t apos[ABATCH], best[ABATCH];
+          // Spatially pruned scan. The host orders the tasks along a Morton curve of their pickup points and
+          // cuts that order into chunks of KCH entries with a bounding box each (static) and a count of
+          // untaken entries (KCNT). Phase A: a chunk with an untaken entry holds one within
+          // lb + diam of an agent (lb: distance to its box), so U_b = min over such chunks of lb + diam
+          // bounds agent b's minimum from above. Phase B: only chunks with lb <= U_b can hold a task at
+          // the minimum distance (ties included); their entries are compared as (distance, task index).
+          uint32_t apos[ABATCH], ub[ABATCH];
 #pragma unroll
           for (uint32_t b = 0; b < ABATCH; ++b) {
             apos[b] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b < B ? s_apos[b] : 0u));
-            best[b] = 0xFFFFFFFFu;
+            ub[b] = 0xFFFFFFFFu;
           }
-          uint64_t best64 = ~0ull;  // !k32: agent 0 only
-          auto visit = [&](uint32_t xy, uint32_t t) {
-            const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
-            if (k32) {
-              const uint32_t tk = (xy == TASK_TAKEN ? 0xFFFFFFFFu : 0u) | t;
-#pragma unroll
-              for (uint32_t b = 0; b < ABATCH; ++b) {
-                if (b >= B) break;  // block-uniform
-                const uint32_t d = __usad(apos[b] & 0xFFFFu, tx, __usad(apos[b] >> 16, ty, 0u));  // v_sad_u32
-                best[b] = min(best[b], (min(d, dsat) << ksh) | tk);
-              }
-            } else {
-              const uint32_t d = __usad(apos[0] & 0xFFFFu, tx, __usad(apos[0] >> 16, ty, 0u));
-              const uint64_t key = xy == TASK_TAKEN ? ~0ull : (((uint64_t)d << 32) | t);
-              best64 = key < best64 ? key : best64;
-            }
+          auto box_lb = [](uint32_t pa, uint32_t lo, uint32_t hi) -> uint32_t {  // distance from pa to a box
+            const uint32_t px = pa & 0xFFFFu, py = pa >> 16;
+            const uint32_t x0 = lo & 0xFFFFu, y0 = lo >> 16, x1 = hi & 0xFFFFu, y1 = hi >> 16;
+            const uint32_t dx = px < x0 ? x0 - px : (px > x1 ? px - x1 : 0u);
+            const uint32_t dy = py < y0 ? y0 - py : (py > y1 ? py - y1 : 0u);
+            return dx + dy;
           };
-          const uint32_t Bs = k32 ? B : 1u;
-          if (P.tasks_lds) {
-            for (uint32_t t = tid; t < P.m; t += bd) visit(S.LIVE[t], t);
-          } else {
-            // 16-B vectors from global memory (P.live: global loads, not flat), lane-interleaved — one
-            // coalesced 1 KB read per wave per vector — four in flight
-            const uint4* L4 = reinterpret_cast<const uint4*>(P.live);
-            constexpr uint32_t VL = 4u;
-            for (uint32_t j0 = tid; j0 < q4; j0 += VL * bd) {
-              uint4 a[VL];
+          // a thread's first KPT chunks (every chunk while kchunks <= KPT * block) are loaded once, all
+          // loads in flight together, and kept in registers for phase B; any further chunks are re-read
+          const uint32_t nch = P.kchunks;
+          uint32_t kc[KPT];
+          uint2 kb[KPT];
 #pragma unroll
-              for (uint32_t u = 0; u < VL; ++u)
-                a[u] = j0 + u * bd < q4 ? L4[j0 + u * bd] : make_uint4(TASK_TAKEN, TASK_TAKEN, TASK_TAKEN, TASK_TAKEN);
-#pragma unroll
-              for (uint32_t u = 0; u < VL; ++u) {
-                const uint32_t t4 = (j0 + u * bd) * 4u;
-                visit(a[u].x, t4);
-                visit(a[u].y, t4 + 1u);
-                visit(a[u].z, t4 + 2u);
-                visit(a[u].w, t4 + 3u);
-              }
-            }
+          for (uint32_t s = 0; s < KPT; ++s) {
+            const uint32_t c = tid + s * bd;
+            kc[s] = c < nch ? P.kcnt[c] : 0u;
+            kb[s] = c < nch ? P.kbox[c] : make_uint2(0u, 0u);
           }
-          if (k32) {
+          auto ub_chunk = [&](uint32_t cnt, uint2 bx) {
+            if (cnt == 0u) return;
+            const uint32_t diam = ((bx.y & 0xFFFFu) - (bx.x & 0xFFFFu)) + ((bx.y >> 16) - (bx.x >> 16));
 #pragma unroll
             for (uint32_t b = 0; b < ABATCH; ++b) {
               if (b >= B) break;  // block-uniform
-              const uint32_t wm = __ockl_wfred_min_u32(best[b]);
-              if (lane == 0 && wm != 0xFFFFFFFFu) atomicMin(&s_bestk32[b], wm);
+              ub[b] = min(ub[b], box_lb(apos[b], bx.x, bx.y) + diam);
             }
-          } else {
-            const uint64_t wm = wave_min_u64(best64);
-            if (lane == 0 && wm != ~0ull) atomicMin(reinterpret_cast<unsigned long long*>(&s_bestk[0]), wm);
+          };
+#pragma unroll
+          for (uint32_t s = 0; s < KPT; ++s) ub_chunk(kc[s], kb[s]);
+          for (uint32_t c = tid + KPT * bd; c < nch; c += bd) ub_chunk(P.kcnt[c], P.kbox[c]);
+#pragma unroll
+          for (uint32_t b = 0; b < ABATCH; ++b) {
+            if (b >= B) break;
+            const uint32_t wm = __ockl_wfred_min_u32(ub[b]);
+            if (lane == 0) atomicMin(&s_ub[b], wm);
+          }
+          __syncthreads();
+          uint32_t bdst[ABATCH], btsk[ABATCH];
+#pragma unroll
+          for (uint32_t b = 0; b < ABATCH; ++b) {
+            ub[b] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b < B ? s_ub[b] : 0u));
+            bdst[b] = 0xFFFFFFFFu;
+            btsk[b] = 0xFFFFFFFFu;
+          }
+          auto scan_chunk = [&](uint32_t c, uint32_t cnt, uint2 bx) {
+            if (cnt == 0u) return;
+            uint32_t mask = 0;
+#pragma unroll
+            for (uint32_t b = 0; b < ABATCH; ++b)
+              if (b < B && box_lb(apos[b], bx.x, bx.y) <= ub[b]) mask |= 1u << b;
+            if (mask == 0u) return;
+            const uint4* L4 = reinterpret_cast<const uint4*>(P.live + (size_t)c * KCH);
+            const uint4* T4 = reinterpret_cast<const uint4*>(P.klt + (size_t)c * KCH);
+#pragma unroll 1
+            for (uint32_t h = 0; h < KCH / 16u; ++h) {  // 16 entries (4 vectors of each array) at a time
+              uint4 xa[4], ta[4];
+#pragma unroll
+              for (uint32_t u = 0; u < 4u; ++u) {
+                xa[u] = L4[4u * h + u];
+                ta[u] = T4[4u * h + u];
+              }
+#pragma unroll
+              for (uint32_t u = 0; u < 4u; ++u) {
+                const uint32_t xs[4] = {xa[u].x, xa[u].y, xa[u].z, xa[u].w};
+                const uint32_t ts[4] = {ta[u].x, ta[u].y, ta[u].z, ta[u].w};
+#pragma unroll
+                for (uint32_t e = 0; e < 4u; ++e) {
+                  const uint32_t xy = xs[e], t = ts[e];
+                  if (xy == TASK_TAKEN) continue;
+                  const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
+#pragma unroll
+                  for (uint32_t b = 0; b < ABATCH; ++b) {
+                    if (b >= B) break;  // block-uniform
+                    if (!((mask >> b) & 1u)) continue;
+                    const uint32_t d = __usad(apos[b] & 0xFFFFu, tx, __usad(apos[b] >> 16, ty, 0u));
+                    const bool lt = d < bdst[b] || (d == bdst[b] && t < btsk[b]);
+                    bdst[b] = lt ? d : bdst[b];
+                    btsk[b] = lt ? t : btsk[b];
+                  }
+                }
+              }
+            }
+          };
+#pragma unroll
+          for (uint32_t s = 0; s < KPT; ++s) scan_chunk(tid + s * bd, kc[s], kb[s]);
+          for (uint32_t c = tid + KPT * bd; c < nch; c += bd) scan_chunk(c, P.kcnt[c], P.kbox[c]);
+#pragma unroll
+          for (uint32_t b = 0; b < ABATCH; ++b) {
+            if (b >= B) break;  // block-uniform
+            const uint32_t dm = __ockl_wfred_min_u32(bdst[b]);
+            const uint32_t tm = __ockl_wfred_min_u32(bdst[b] == dm ? btsk[b] : 0xFFFFFFFFu);
+            if (lane == 0 && dm != 0xFFFFFFFFu)
+              atomicMin(reinterpret_cast<unsigned long long*>(&s_bestk[b]), ((unsigned long long)dm << 32) | tm);
           }
           __syncthreads();
           PLAN_TICK(34);
           if (tid == 0) {
             uint32_t acc = 0, stop = 0;
-            const uint32_t Bk = P.key32 ? B : 1u;
-            if (P.key32)  // 32-bit keys -> (distance, task) as the u64 path has them
-              for (uint32_t b = 0; b < Bk; ++b)
-                s_bestk[b] = s_bestk32[b] == 0xFFFFFFFFu ? ~0ull : (uint64_t)(s_bestk32[b] & ((1u << P.kshift) - 1u));
-            for (uint32_t b = 0; b < Bk; ++b) {
+            for (uint32_t b = 0; b < B; ++b) {
               if (list[kk + b] > bad_at || s_ctl.unused == 0u || s_bestk[b] == ~0ull) {
                 stop = 1;  // past the first bad delivery / out of tasks: this step assigns no more
                 break;
@@ -1155,10 +1204,18 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
           const uint32_t acc = s_cnt2;
           if (tid < acc) {  // the accepted agents' updates in parallel (tswap.rs:132-136)
             const uint32_t ai = list[kk + tid], t = s_acct[tid];
-            S.LIVE[t] = TASK_TAKEN;
-            if (P.tasks_lds) P.live[t] = TASK_TAKEN;
+            const uint32_t pos = P.kpos[t];  // the task's entry in the Morton order
+            P.live[pos] = TASK_TAKEN;
+            atomicSub(&P.kcnt[pos / KCH], 1u);
             P.task[ai] = (int32_t)t;
             P.st[ai] = ST_TO_PICKUP;
+            if (P.pred) {  // diagnostics: was this the task last predicted for the agent?
+              atomicAdd(&P.cc->pred_asg, 1u);
+              const uint32_t pt = ld_agent(&P.pred[ai]);
+              if (pt == t) atomicAdd(&P.cc->pred_hit, 1u);
+              else if (pt == 0xFFFFFFFFu) atomicAdd(&P.cc->pred_none, 1u);
+              __hip_atomic_store(&P.pred[ai], 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             if (P.dbg) S.DEC[ai] = 0x40;
             DTAG(ai, 16u);
             const uint32_t ng = P.pick[t];

@@ -45,7 +45,8 @@ __device__ __forceinline__ uint32_t hw_xcc_id() {
   return (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID[3:0]
 }
 
-// lane 0: claim the next pair (0: needed queue, 1: speculative queue, 2: task chain, -1: exit).
+// lane 0: claim the next pair (0: needed queue, 1: speculative queue, 2: task chain, 3: hot task chain,
+// 4: predicted task chain, -1: exit).
 // Task chains (long, lowest priority) only go to workers with take_t: the others stay free for the
 // pairs the planner needs or will need soon.
 __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool take_t, const uint32_t* hflags,
@@ -85,6 +86,15 @@ __device__ __forceinline__ int worker_claim(CoopCtl* cc, uint32_t* idx, bool tak
           if (w_cas(&cc->claim_h, ch, ch + 1u)) {
             *idx = ch;
             return 3;
+          }
+          continue;
+        }
+        // then predicted chains: tasks agents are about to be assigned
+        const uint32_t hp = w_ld(&cc->head_p), cp = w_ld(&cc->claim_p);
+        if (cp < hp) {
+          if (w_cas(&cc->claim_p, cp, cp + 1u)) {
+            *idx = cp;
+            return 4;
           }
           continue;
         }
@@ -355,6 +365,39 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     return __builtin_amdgcn_readfirstlane(drop ? 1 : 0) != 0;
   };
   const bool take_t = (wid & A.tmask) == A.tmask;
+  // the task an agent idle at cell D will be assigned if nothing changes before: the untaken task whose
+  // pickup is nearest to D, first by task index on ties (tswap.rs:123-130 as K4 computes it) — read from
+  // K4's spatial index while the planner updates it, so a prediction can be stale; it only picks a chain
+  auto predict_task = [&](uint32_t D) -> uint32_t {
+    const uint32_t dy = D / G.W, dx = D - dy * G.W, nch = A.kchunks;
+    auto box_lb = [&](uint2 bx) -> uint32_t {
+      const uint32_t x0 = bx.x & 0xFFFFu, y0 = bx.x >> 16, x1 = bx.y & 0xFFFFu, y1 = bx.y >> 16;
+      return (dx < x0 ? x0 - dx : dx > x1 ? dx - x1 : 0u) + (dy < y0 ? y0 - dy : dy > y1 ? dy - y1 : 0u);
+    };
+    uint32_t ub = 0xFFFFFFFFu;
+    for (uint32_t c = lane; c < nch; c += 64u) {
+      if (w_ld(&A.kcnt[c]) == 0u) continue;
+      const uint2 bx = A.kbox[c];
+      ub = min(ub, box_lb(bx) + ((bx.y & 0xFFFFu) - (bx.x & 0xFFFFu)) + ((bx.y >> 16) - (bx.x >> 16)));
+    }
+    ub = __ockl_wfred_min_u32(ub);
+    uint32_t bdst = 0xFFFFFFFFu, btsk = 0xFFFFFFFFu;
+    for (uint32_t c = lane; c < nch; c += 64u) {
+      if (w_ld(&A.kcnt[c]) == 0u || box_lb(A.kbox[c]) > ub) continue;
+      for (uint32_t e = 0; e < 32u; ++e) {
+        const uint32_t xy = w_ld(&A.klive[c * 32u + e]);
+        if (xy == 0xFFFFFFFFu) continue;
+        const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
+        const uint32_t d = (tx > dx ? tx - dx : dx - tx) + (ty > dy ? ty - dy : dy - ty), t = A.klt[c * 32u + e];
+        if (d < bdst || (d == bdst && t < btsk)) {
+          bdst = d;
+          btsk = t;
+        }
+      }
+    }
+    const uint32_t dm = __ockl_wfred_min_u32(bdst);
+    return __ockl_wfred_min_u32(bdst == dm ? btsk : 0xFFFFFFFFu);
+  };
   for (;;) {
     int which = -1;
     uint32_t idx = 0;
@@ -365,10 +408,23 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     // the entry was published by the planner's release of the head (or by the host before the
     // launch): read it past stale caches
     const uint32_t* e =
-        reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : which == 3 ? A.QH : A.QT) + idx);
-    if (which == 3) which = 2;  // a hot chain is walked as any task chain
-    const uint32_t v = w_ld(e), goal = w_ld(e + 1);
-    const int32_t tab = (int32_t)w_ld(e + 2);
+        which == 4 ? reinterpret_cast<const uint32_t*>(A.QP + idx)
+                   : reinterpret_cast<const uint32_t*>((which == 0 ? A.QN : which == 1 ? A.QS : which == 3 ? A.QH : A.QT) + idx);
+    uint32_t v = w_ld(e), goal = w_ld(e + 1);
+    int32_t tab = which == 4 ? -1 : (int32_t)w_ld(e + 2);  // a QP entry is two words
+    if (which == 4) {  // predicted chain: entry = (delivery cell, agent)
+      const uint32_t t = predict_task(v);
+      if (lane == 0) {
+        __hip_atomic_fetch_add(&A.cc->pred_jobs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (A.pred) __hip_atomic_store(&A.pred[goal], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (t == 0xFFFFFFFFu) continue;
+      v = A.pick[t];
+      goal = A.dlv[t];
+      if (v == CELL_BAD || goal == CELL_BAD || v == goal) continue;
+      tab = A.goal_tab[goal];
+    }
+    if (which >= 3) which = 2;  // hot and predicted chains are walked as any task chain
     cur_q = (uint32_t)which;
     if (which < 2) {
       // a pair resolved meanwhile (a promoted speculative pair whose first copy finished, or a chain
