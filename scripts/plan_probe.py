@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--diag", action="store_true")
     ap.add_argument("--reps", type=int, default=2)
     a = ap.parse_args()
-    rows, starts, tasks = maps.config_instance(a.config)
+    rows, starts, tasks = maps.wh10k_instance() if a.config == "wh10k" else maps.config_instance(a.config)
     with Planner(rows, diag=a.diag) as p:
         p.plan_mapd_arrays(starts, tasks, 50)  # warm-up
         for T in a.horizons:
