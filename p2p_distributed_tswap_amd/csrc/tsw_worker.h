@@ -367,7 +367,9 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
   const bool take_t = (wid & A.tmask) == A.tmask;
   // the task an agent idle at cell D will be assigned if nothing changes before: the untaken task whose
   // pickup is nearest to D, first by task index on ties (tswap.rs:123-130 as K4 computes it) — read from
-  // K4's spatial index while the planner updates it, so a prediction can be stale; it only picks a chain
+  // K4's spatial index while the planner updates it, with plain loads (this XCD's L2 copy may be stale: a
+  // prediction only picks a chain, and agent-scope loads of the whole chunk-count array for every
+  // prediction moved ~128 KB each past the L2)
   auto predict_task = [&](uint32_t D) -> uint32_t {
     const uint32_t dy = D / G.W, dx = D - dy * G.W, nch = A.kchunks;
     auto box_lb = [&](uint2 bx) -> uint32_t {
@@ -376,16 +378,16 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     };
     uint32_t ub = 0xFFFFFFFFu;
     for (uint32_t c = lane; c < nch; c += 64u) {
-      if (w_ld(&A.kcnt[c]) == 0u) continue;
+      if (A.kcnt[c] == 0u) continue;
       const uint2 bx = A.kbox[c];
       ub = min(ub, box_lb(bx) + ((bx.y & 0xFFFFu) - (bx.x & 0xFFFFu)) + ((bx.y >> 16) - (bx.x >> 16)));
     }
     ub = __ockl_wfred_min_u32(ub);
     uint32_t bdst = 0xFFFFFFFFu, btsk = 0xFFFFFFFFu;
     for (uint32_t c = lane; c < nch; c += 64u) {
-      if (w_ld(&A.kcnt[c]) == 0u || box_lb(A.kbox[c]) > ub) continue;
+      if (A.kcnt[c] == 0u || box_lb(A.kbox[c]) > ub) continue;
       for (uint32_t e = 0; e < 32u; ++e) {
-        const uint32_t xy = w_ld(&A.klive[c * 32u + e]);
+        const uint32_t xy = A.klive[c * 32u + e];
         if (xy == 0xFFFFFFFFu) continue;
         const uint32_t tx = xy & 0xFFFFu, ty = xy >> 16;
         const uint32_t d = (tx > dx ? tx - dx : dx - tx) + (ty > dy ? ty - dy : dy - ty), t = A.klt[c * 32u + e];
@@ -397,6 +399,36 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     }
     const uint32_t dm = __ockl_wfred_min_u32(bdst);
     return __ockl_wfred_min_u32(bdst == dm ? btsk : 0xFFFFFFFFu);
+  };
+  auto walk_chain = [&](uint32_t c, uint32_t goal, int32_t tab) {
+    const uint32_t max_hops = A.chain_hops ? A.chain_hops : ncell;
+    for (uint32_t hop = 0; hop < max_hops && c != goal; ++hop) {
+      // the planner is done: abandon the rest of the chain (nothing is marked pending)
+      if ((uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? w_ld(&A.cc->stop) : 0u)) break;
+      // pairs the planner queued meanwhile come first (A.preempt)
+      while (A.preempt) {
+        int w2 = -1;
+        uint32_t i2 = 0;
+        if (lane == 0) w2 = worker_try_claim(A.cc, &i2);
+        w2 = __builtin_amdgcn_readfirstlane(w2);
+        if (w2 < 0) break;
+        i2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i2);
+        const uint32_t* e2 = reinterpret_cast<const uint32_t*>((w2 == 0 ? A.QN : A.QS) + i2);
+        const uint32_t v2 = w_ld(e2), g2 = w_ld(e2 + 1);
+        const int32_t t2 = (int32_t)w_ld(e2 + 2);
+        if (w2 == 1 && drop_stale(e2, v2, t2)) continue;
+        cur_q = (uint32_t)w2;
+        publish_code(v2, t2, resolve(v2, g2, t2), false);
+        cur_q = 2u;
+      }
+      uint8_t code = (uint8_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(c, tab) : 0u);
+      if (code == NH_UNKNOWN) {
+        code = resolve(c, goal, tab);
+        publish_code(c, tab, code, true);
+      }
+      if (code >= NH_STAY) break;  // stay (unreachable goal), pending elsewhere, or overflow
+      c = step_cell(c, code, G.W);
+    }
   };
   for (;;) {
     int which = -1;
@@ -448,35 +480,7 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     // resolve each unresolved hop in turn; stop at a pair someone else has queued, at a stay code,
     // or at the goal. Pairs are not marked pending, so an abandoned chain leaves nothing behind.
     if (tab < 0) continue;
-    uint32_t c = v;
-    const uint32_t max_hops = A.chain_hops ? A.chain_hops : ncell;
-    for (uint32_t hop = 0; hop < max_hops && c != goal; ++hop) {
-      // the planner is done: abandon the rest of the chain (nothing is marked pending)
-      if ((uint32_t)__builtin_amdgcn_readfirstlane(lane == 0 ? w_ld(&A.cc->stop) : 0u)) break;
-      // pairs the planner queued meanwhile come first (A.preempt)
-      while (A.preempt) {
-        int w2 = -1;
-        uint32_t i2 = 0;
-        if (lane == 0) w2 = worker_try_claim(A.cc, &i2);
-        w2 = __builtin_amdgcn_readfirstlane(w2);
-        if (w2 < 0) break;
-        i2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i2);
-        const uint32_t* e2 = reinterpret_cast<const uint32_t*>((w2 == 0 ? A.QN : A.QS) + i2);
-        const uint32_t v2 = w_ld(e2), g2 = w_ld(e2 + 1);
-        const int32_t t2 = (int32_t)w_ld(e2 + 2);
-        if (w2 == 1 && drop_stale(e2, v2, t2)) continue;
-        cur_q = (uint32_t)w2;
-        publish_code(v2, t2, resolve(v2, g2, t2), false);
-        cur_q = 2u;
-      }
-      uint8_t code = (uint8_t)__builtin_amdgcn_readfirstlane(lane == 0 ? code_at(c, tab) : 0u);
-      if (code == NH_UNKNOWN) {
-        code = resolve(c, goal, tab);
-        publish_code(c, tab, code, true);
-      }
-      if (code >= NH_STAY) break;  // stay (unreachable goal), pending elsewhere, or overflow
-      c = step_cell(c, code, G.W);
-    }
+    walk_chain(v, goal, tab);
   }
   if (lane == 0) {
     A.epochs[wid] = ep;
