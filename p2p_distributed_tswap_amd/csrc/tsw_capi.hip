@@ -70,6 +70,7 @@ struct Tunables {
   uint32_t wide_hi = 16, wide_lo = 4;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops with a small / large speculative backlog
   bool hot_chains = true;         // TSW_HOT_CHAINS=0: no planner-fed chains of just-assigned tasks (A/B)
   uint32_t chain_hops = 0;        // TSW_CHAIN_HOPS: hops resolved per task chain (0: the whole path)
+  bool walk_cache = true;         // TSW_WALK_CACHE=0: the step-start walk-ahead re-reads every code from the agent's next cell
   uint32_t predict = 1;           // TSW_PREDICT: predicted task chains, bit 0 at pickups, bit 1 at delivery-goal changes (0: off)
   uint32_t urgent_hops = 1;       // TSW_URGENT_HOPS: walk-ahead pairs this close are queued as needed (0: off)
   uint32_t dag_width = 4;         // TSW_DAG_WIDTH: cells per DAG prefetch level (<= 16)
@@ -133,6 +134,7 @@ struct Tunables {
     t.chain_hops = (uint32_t)num("TSW_CHAIN_HOPS", 0, 1000000, t.chain_hops);
     t.hot_chains = num("TSW_HOT_CHAINS", 0, 1, t.hot_chains ? 1 : 0) != 0;
     t.predict = (uint32_t)num("TSW_PREDICT", 0, 3, t.predict);
+    t.walk_cache = num("TSW_WALK_CACHE", 0, 1, 1) != 0;
     t.ab_flags = (uint32_t)num("TSW_AB_FLAGS", 0, 255, t.ab_flags);
     t.t0_delay_us = (uint32_t)num("TSW_T0_DELAY_US", 0, 10000000, t.t0_delay_us);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
@@ -250,6 +252,8 @@ struct tsw_ctx {
   uint2* d_QP = nullptr;         // predicted task chains (planner-filled at pickups), PlanArgs::QP
   size_t qpcap = 0;
   uint32_t* d_pred = nullptr;    // TSW_PLAN_DEBUG: per-agent last predicted task
+  uint4* d_wf = nullptr;         // per-agent walk-ahead frontier (PlanArgs::wf)
+  size_t wfcap = 0;
   size_t predcap = 0;
   size_t qtcap = 0;
   uint32_t qt_count = 0;
@@ -1308,6 +1312,16 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
     }
     if (c->d_dtag && hipMemsetAsync(c->d_dtag, 0, (size_t)n * 4, c->s) == hipSuccess) P.dtag = c->d_dtag;
   }
+  P.wf = nullptr;
+  if (c->tun.walk_cache && n) {  // re-armed per plan / step call (a goal never matches 0xFFFFFFFF)
+    if (c->wfcap < n) {
+      if (c->d_wf) (void)hipFree(c->d_wf);
+      c->d_wf = nullptr;
+      c->wfcap = 0;
+      if (hipMalloc(&c->d_wf, (size_t)n * sizeof(uint4)) == hipSuccess) c->wfcap = n;
+    }
+    if (c->d_wf && hipMemsetAsync(c->d_wf, 0xFF, (size_t)n * sizeof(uint4), c->s) == hipSuccess) P.wf = c->d_wf;
+  }
   P.pred = nullptr;
   if (P.dbg && n && mode == MODE_MAPD) {  // diagnostics only: prediction hits
     if (c->predcap < n) {
@@ -2024,7 +2038,7 @@ void tsw_destroy(tsw_ctx* c) {
   if (c->h_dups) (void)hipHostFree(c->h_dups);
   fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_dtag); fre(c->d_live); fre(c->d_klt); fre(c->d_kpos); fre(c->d_kbox); fre(c->d_kcnt); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
-  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_QH); fre(c->d_QP); fre(c->d_pred); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
+  fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_QH); fre(c->d_QP); fre(c->d_pred); fre(c->d_wf); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
   if (c->h_cc) (void)hipHostFree(c->h_cc);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->h_stat) hipHostFree(c->h_stat);

@@ -114,6 +114,7 @@ struct PlanArgs {
   uint32_t qpcap;
   uint32_t predict;     // bit 0: at pickups, bit 1: at goal changes of delivering agents
   uint32_t* pred;       // diagnostics (TSW_PLAN_DEBUG): per agent, the task last predicted for it
+  uint4* wf;            // per agent: step-start walk-ahead frontier (cell at the walk, goal, stopping cell, its hop); nullptr: off
   CoopCtl* cc;
   // host-visible (pinned, system-coherent) words: [0] set when the planner block is resident,
   // [1] abort (host watchdog: planner waits give up, workers exit), [2] planner heartbeat (timesteps)

@@ -558,7 +558,8 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
 // only their goals, hence their next hops and successors, moved, so only their pairs are new.
 // After rules_init (SUCC valid).
 __device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab,
-                                  uint32_t hops);
+                                  uint32_t hops, uint32_t h0 = 0u, uint32_t* end = nullptr,
+                                  uint32_t* endh = nullptr);
 __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab);
 
 // coop mode: agent k will be idle at `cell` (its delivery): a worker predicts its next task and walks that
@@ -651,12 +652,18 @@ __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint3
   }
 }
 
-// Walk the resolved codes toward g from cell u for at most `hops` cells; queue the first unresolved
-// pair (and the DAG past it). Returns the hops left when the walk reached g, else 0.
+// Walk the resolved codes toward g from cell u, which lies h0 resolved hops past the agent's next cell,
+// until hop `hops`; queue the first unresolved pair (and the DAG past it). Returns the hops left when the
+// walk reached g, else 0. *end / *endh (if given): the cell the walk stopped at and its hop index.
 __device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab,
-                                  uint32_t hops) {
-  for (uint32_t h = 0; h < hops; ++h) {
-    if (u == g) return hops - h;
+                                  uint32_t hops, uint32_t h0, uint32_t* end, uint32_t* endh) {
+  uint32_t h = h0;
+  uint32_t left = 0;
+  for (; h < hops; ++h) {
+    if (u == g) {
+      left = hops - h;
+      break;
+    }
     const uint8_t cu = P.nh[(uint64_t)tab * P.nstride + u];
     if (cu == NH_UNKNOWN || cu == NH_PENDING || cu == NH_PENDING_S) {
       // a pair the agent reads within urgent_hops steps goes to the needed queue (served before the
@@ -664,12 +671,16 @@ __device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, 
       if (P.coop && h < P.urgent_hops) enqueue_pair(P, u, g, tab, s_q);
       else if (cu == NH_UNKNOWN) prefetch_pair(P, u, g, tab, s_q);
       if (P.dag_prefetch) dag_prefetch(P, s_q, u, g, tab);
-      return 0;
+      break;
     }
-    if (cu >= NH_STAY) return 0;  // a stay code
+    if (cu >= NH_STAY) break;  // a stay code
     u = step_cell(u, cu, P.W);
   }
-  return 0;
+  if (end) {
+    *end = u;
+    *endh = h;
+  }
+  return left;
 }
 
 // Parallel: the next hop of every agent from the cell its resolved code points at (the pair the
@@ -714,7 +725,30 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
       if ((P.prefetch_ext & 1u) && P.dag_prefetch) dag_prefetch(P, s_q, S.V[k], S.G[k], tab);
       continue;
     }
-    const uint32_t left = walk_prefetch(P, s_q, step_cell(S.V[k], c, P.W), S.G[k], tab, hops);
+    // Resolved codes never change, so the path from the agent's next cell is fixed while its goal is: the
+    // walk resumes at last step's stopping cell (P.wf: cell at that walk, goal, stopping cell, its hop
+    // index). An agent that moved since went one hop along that path, so the index drops by one.
+    uint32_t u0 = step_cell(S.V[k], c, P.W), h0 = 0;
+    const uint32_t vk = S.V[k], gk = S.G[k];
+    if (P.wf) {
+      const uint4 f = P.wf[k];
+      // moved: exactly one hop along the cached path (goals can change and change back in between)
+      bool on = f.y == gk && f.x == vk;
+      if (f.y == gk && f.x != vk && f.x < P.ncell) {
+        const uint8_t cf = P.nh[(uint64_t)tab * P.nstride + f.x];
+        on = cf < NH_STAY && step_cell(f.x, cf, P.W) == vk;
+      }
+      if (on) {
+        const uint32_t hp = f.x == vk ? f.w : (f.w > 0u ? f.w - 1u : 0u);
+        if (hp > 0u) {
+          u0 = f.z;
+          h0 = hp;
+        }
+      }
+    }
+    uint32_t ue = u0, he = h0;
+    const uint32_t left = h0 >= hops ? 0u : walk_prefetch(P, s_q, u0, gk, tab, hops, h0, &ue, &he);
+    if (P.wf) P.wf[k] = make_uint4(vk, gk, ue, he);
     if (left > 0u && dtab >= 0 && (P.prefetch_ext & 2u)) walk_prefetch(P, s_q, pc, dc, dtab, left);
   }
   __syncthreads();

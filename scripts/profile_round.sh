@@ -26,4 +26,7 @@ for WL in plan plan_exit bfs; do
 done
 # planner / worker traffic split of the coop dispatch (scripts/warm_split.py): cold vs warm plan
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/warm_pmc_fetch -o run -- python3 scripts/warm_plan.py --reps 1 > $OUT/warm_pmc_fetch.json 2> $OUT/warm_pmc_fetch.err &&
-timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/warm_pmc_write -o run -- python3 scripts/warm_plan.py --reps 1 > $OUT/warm_pmc_write.json 2> $OUT/warm_pmc_write.err || exit 1
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/warm_pmc_write -o run -- python3 scripts/warm_plan.py --reps 1 > $OUT/warm_pmc_write.json 2> $OUT/warm_pmc_write.err &&
+# ... and without task chains (diagnostic library, TSW_TASK_CHAINS=0): the warm plan's bytes are then the planner's
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/warmnc_pmc_fetch -o run -- python3 scripts/warm_plan.py --reps 1 --no-chains > $OUT/warmnc_pmc_fetch.json 2> $OUT/warmnc_pmc_fetch.err &&
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/warmnc_pmc_write -o run -- python3 scripts/warm_plan.py --reps 1 --no-chains > $OUT/warmnc_pmc_write.json 2> $OUT/warmnc_pmc_write.err || exit 1

@@ -2,7 +2,9 @@
 every next-hop code the first one resolved still in the table store (no K3 waits), vs cold plans from
 an empty store. cold - warm = what the A* latency chain costs the plan.
 
-usage: python scripts/warm_plan.py [--config c3_warehouse_170x84] [--reps 3]
+usage: python scripts/warm_plan.py [--config c3_warehouse_170x84] [--reps 3] [--no-chains]
+(--no-chains: the diagnostic library with TSW_TASK_CHAINS=0 — no task-chain jobs, whose walks through
+ the resolved store in the warm plan would otherwise count as planner traffic in scripts/warm_split.py)
 """
 import argparse
 import json
@@ -20,11 +22,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3_warehouse_170x84")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--no-chains", action="store_true")
     a = ap.parse_args()
+    if a.no_chains:
+        os.environ["TSW_TASK_CHAINS"] = "0"  # read at tsw_create by the diagnostic library
     rows, starts, tasks = maps.config_instance(a.config)
-    out = {"config": a.config, "build_id": build_id(), "cold_ms": [], "warm_ms": [], "warm_waits": [], "cold_waits": [],
+    out = {"config": a.config, "build_id": build_id(a.no_chains), "task_chains": not a.no_chains, "cold_ms": [], "warm_ms": [], "warm_waits": [], "cold_waits": [],
            "cold_queries": [], "warm_queries": []}
-    with Planner(rows) as p:
+    with Planner(rows, diag=a.no_chains) as p:
         p.plan_mapd_arrays(starts, tasks, 50)
         for _ in range(a.reps):
             p.clear_tables()

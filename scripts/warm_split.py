@@ -8,7 +8,10 @@ counter, the warm dispatch's bytes are the planner's (plus idle polling), and co
 workers' A* moved. Exit-mode profiles cannot give this split: every exit relaunch re-stages the
 planner's state, so the exit-mode planner moves more bytes than the whole fused dispatch.
 
-usage: python scripts/warm_split.py FETCH_DIR WRITE_DIR WARM_JSON OUT_JSON
+usage: python scripts/warm_split.py FETCH_DIR WRITE_DIR WARM_JSON OUT_JSON [NC_FETCH_DIR NC_WRITE_DIR NC_JSON]
+(the optional NC_* passes are `warm_plan.py --reps 1 --no-chains`: without task chains the warm dispatch
+ holds no chain walks through the resolved store, so its bytes are the planner's alone — reported as
+ planner_bytes_per_agent_step when given; the default run's warm figure stays as warm_dispatch_bytes)
 (FETCH_DIR / WRITE_DIR: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE -d outputs of
  `python3 scripts/warm_plan.py --reps 1`; gfx950 correction as in summarize_profile.py:
  read bytes = 2 x FETCH_SIZE KB, write bytes = WRITE_SIZE KB)
@@ -34,6 +37,7 @@ def plan_dispatches(d, counter):
 
 def main():
     fdir, wdir, warm_json, out_path = sys.argv[1:5]
+    nc = sys.argv[5:8] if len(sys.argv) >= 8 else None
     fe, wr = plan_dispatches(fdir, "FETCH_SIZE"), plan_dispatches(wdir, "WRITE_SIZE")
     # dispatch order of warm_plan.py --reps 1: warm-up plan (50 steps), cold plan, warm plan
     if len(fe) != 3 or len(wr) != 3:
@@ -47,6 +51,18 @@ def main():
     cold, warm = bytes_of(1), bytes_of(2)
     q = wj["cold_queries"][0]
     agent_steps = wj.get("agent_steps", 1000 * 2001)  # agents x recorded timesteps of the plan
+    planner = warm
+    planner_src = "warm plan dispatch (task chains on: includes the workers' walks through the resolved store)"
+    if nc:
+        fe2, wr2 = plan_dispatches(nc[0], "FETCH_SIZE"), plan_dispatches(nc[1], "WRITE_SIZE")
+        if len(fe2) != 3 or len(wr2) != 3:
+            raise SystemExit(f"no-chains: expected 3 k_plan dispatches per pass, got {len(fe2)} / {len(wr2)}")
+        with open(nc[2]) as fh:
+            wj2 = json.loads([l for l in fh if l.startswith("{")][-1])
+        if wj2.get("build_id") != wj.get("build_id"):
+            raise SystemExit("no-chains profile of another build")
+        planner = 2.0 * fe2[2][1] * 1024.0 + wr2[2][1] * 1024.0
+        planner_src = "warm plan dispatch without task chains (diagnostic library, TSW_TASK_CHAINS=0)"
     out = {
         "config": wj["config"],
         "build_id": wj.get("build_id"),
@@ -55,7 +71,9 @@ def main():
         "warm_dispatch_bytes": round(warm),
         "cold_dispatch_ms": round(fe[1][2] / 1e6, 2),
         "warm_dispatch_ms": round(fe[2][2] / 1e6, 2),
-        "planner_bytes_per_agent_step": round(warm / agent_steps, 1),
+        "planner_bytes_per_agent_step": round(planner / agent_steps, 1),
+        "planner_bytes_source": planner_src,
+        "warm_dispatch_bytes_per_agent_step": round(warm / agent_steps, 1),
         "planner_algorithmic_bytes_per_agent_step": 46.0,
         "workers_bytes": round(cold - warm),
         "worker_queries": q,
