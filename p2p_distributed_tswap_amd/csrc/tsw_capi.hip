@@ -1346,7 +1346,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   bool fl = !ag && c->tun.flinks_lds && plan_lds_bytes(n, P.ncell, m, false, false, false, true, true, part) <= budget;
   // the occupancy grid with the movement rounds' MU words, else OCC alone (every rules round reads
   // OCC: C3's 170x84 fits OCC but not MU beside the agent arrays)
-  bool mu = plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, true, part) <= budget;
+  bool mu = n < 65535u && plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, true, part) <= budget;  // MU32: 16-bit agent ids
   bool oc = mu || (c->tun.occ_split && plan_lds_bytes(n, P.ncell, m, ag, true, false, fl, false, part) <= budget);
   const bool tk = false;  // K4 reads its spatial index from global memory (the chunks it needs only)
   P.part_lds = part;

@@ -91,6 +91,7 @@ struct Arrays {
   uint32_t* F2;
   uint32_t* OCC;   // per cell: lowest agent | OCC_FLAG, or OCC_NONE
   uint64_t* MU;    // per cell: (round << 32) | ~(lowest undecided agent targeting it), movement rounds
+  uint32_t* MU32;  // the same in LDS (MUL, n < 2^16): round16 << 16 | (0xFFFF - agent), round16 in [1, 65535]
   uint32_t* LIVE;  // K4: pickup points in Morton order, TASK_TAKEN once assigned (PlanArgs::live)
   unsigned long long t0;  // wall clock at the launch (coop: "no worker has started" is measured from here)
 };
@@ -919,8 +920,12 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
   }
   if constexpr (OC) {
     S.OCC = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
-    if constexpr (MUL) S.MU = reinterpret_cast<uint64_t*>(carve((size_t)P.ncell * 8));
-    else S.MU = P.mu;
+    if constexpr (MUL) {
+      S.MU32 = reinterpret_cast<uint32_t*>(carve((size_t)P.ncell * 4));
+      S.MU = nullptr;
+    } else {
+      S.MU = P.mu;
+    }
   } else {
     S.OCC = P.occ;
     S.MU = P.mu;
@@ -943,7 +948,10 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
   if constexpr (OC)
     for (uint32_t c = tid; c < P.ncell; c += bd) S.OCC[c] = P.occ[c];
   // round tags start at 1 (move_rounds is incremented before use), so zeroed MU is stale
-  for (uint32_t c = tid; c < P.ncell; c += bd) S.MU[c] = 0ull;
+  for (uint32_t c = tid; c < P.ncell; c += bd) {
+    if constexpr (MUL) S.MU32[c] = 0u;
+    else S.MU[c] = 0ull;
+  }
   if (tid == 0) {
     s_ctl = *P.ctl;
     s_ctl.status = PLAN_RUNNING;
@@ -2159,6 +2167,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       // Round passes as per-agent bodies, run either block-wide (k = tid, tid + bd, ...) or, in
       // the tail, by wave 0 alone over a compact list of the still-open agents.
       uint64_t tag = 0;
+      uint32_t tag16 = 0;  // MUL: the round's 16-bit tag (1..65535; MU32 is cleared when it wraps to 1)
+      auto set_tag = [&](uint32_t r) {
+        tag = (uint64_t)r << 32;
+        tag16 = (r - 1u) % 65535u + 1u;
+      };
       // pass 1: target cell of an open agent; MU[c] = lowest open agent targeting c, as a
       // round-tagged max of ~k (no reset pass: entries of older rounds are stale)
       auto pass1 = [&](uint32_t k) -> bool {
@@ -2173,12 +2186,18 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         }
         const uint32_t u = step_cell(S.V[k], (uint32_t)code, W);
         S.SUCC[k] = u;
-        atomicMax(reinterpret_cast<unsigned long long*>(&S.MU[u]), (unsigned long long)(tag | (uint32_t)~k));
+        if constexpr (MUL) atomicMax(&S.MU32[u], (tag16 << 16) | (0xFFFFu - k));
+        else atomicMax(reinterpret_cast<unsigned long long*>(&S.MU[u]), (unsigned long long)(tag | (uint32_t)~k));
         return true;
       };
       auto mu_of = [&](uint32_t c) -> uint32_t {  // lowest open agent targeting c this round
-        const uint64_t x = S.MU[c];
-        return (x >> 32) == (tag >> 32) ? ~(uint32_t)x : NO_AGENT;
+        if constexpr (MUL) {
+          const uint32_t x = S.MU32[c];
+          return (x >> 16) == tag16 ? 0xFFFFu - (x & 0xFFFFu) : NO_AGENT;
+        } else {
+          const uint64_t x = S.MU[c];
+          return (x >> 32) == (tag >> 32) ? ~(uint32_t)x : NO_AGENT;
+        }
       };
       // pass 2: tentatively decide an open agent whose turn can be replayed from the round-start
       // state. What k reads at its turn is OCC[u] (u = its target), the occupant j's cell, goal
@@ -2268,7 +2287,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
         }
         __syncthreads();
         if (s_abort) break;
-        tag = (uint64_t)s_ctl.move_rounds << 32;
+        set_tag(s_ctl.move_rounds);
+        if (MUL && tag16 == 1u && s_ctl.move_rounds > 1u) {  // the 16-bit tag wrapped: old entries would match
+          for (uint32_t c = tid; c < P.ncell; c += bd) S.MU32[c] = 0u;
+          __syncthreads();
+        }
         int open = 0;
         for (uint32_t k = tid; k < n; k += bd) open |= pass1(k) ? 1 : 0;
         // one agent per thread: the count is exact and decides the switch to the wave tail
@@ -2318,7 +2341,11 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
               __threadfence_block();
               if (*(volatile uint32_t*)&s_abort) break;
               __threadfence_block();
-              tag = (uint64_t)(*(volatile uint32_t*)&s_ctl.move_rounds) << 32;
+              set_tag(*(volatile uint32_t*)&s_ctl.move_rounds);
+              if (MUL && tag16 == 1u) {  // wrapped (wave 0 alone here)
+                for (uint32_t c = lane; c < P.ncell; c += 64u) S.MU32[c] = 0u;
+                __threadfence_block();
+              }
               const bool op = kk != NO_AGENT && pass1(kk);
               __threadfence_block();
               if (__ballot(op) == 0ull) break;
@@ -2474,7 +2501,7 @@ size_t plan_lds_bytes(uint32_t n, uint32_t ncell, uint32_t m, bool agents, bool 
     b += part_lds_bytes(n, part);
     if (flinks) b += 2 * r16((size_t)(n + 1) * 4);
   }
-  if (occ) b += r16((size_t)ncell * 4) + (mu ? r16((size_t)ncell * 8) : 0u);
+  if (occ) b += r16((size_t)ncell * 4) + (mu ? r16((size_t)ncell * 4) : 0u);  // MU in LDS: u32 words (MU32)
   if (tasks) b += r16((size_t)((m + 3u) & ~3u) * 4);
   return b;
 }
