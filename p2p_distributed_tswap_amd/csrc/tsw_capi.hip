@@ -70,6 +70,7 @@ struct Tunables {
   uint32_t wide_hi = 16, wide_lo = 4;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops with a small / large speculative backlog
   bool hot_chains = true;         // TSW_HOT_CHAINS=0: no planner-fed chains of just-assigned tasks (A/B)
   uint32_t chain_hops = 0;        // TSW_CHAIN_HOPS: hops resolved per task chain (0: the whole path)
+  uint32_t move_round0 = 0;       // TSW_MOVE_ROUND0 (test knob): movement-round counter at the plan start (forces the MU32 tag wrap)
   bool walk_cache = true;         // TSW_WALK_CACHE=0: the step-start walk-ahead re-reads every code from the agent's next cell
   uint32_t predict = 1;           // TSW_PREDICT: predicted task chains, bit 0 at pickups, bit 1 at delivery-goal changes (0: off)
   uint32_t urgent_hops = 1;       // TSW_URGENT_HOPS: walk-ahead pairs this close are queued as needed (0: off)
@@ -135,6 +136,7 @@ struct Tunables {
     t.hot_chains = num("TSW_HOT_CHAINS", 0, 1, t.hot_chains ? 1 : 0) != 0;
     t.predict = (uint32_t)num("TSW_PREDICT", 0, 3, t.predict);
     t.walk_cache = num("TSW_WALK_CACHE", 0, 1, 1) != 0;
+    t.move_round0 = (uint32_t)num("TSW_MOVE_ROUND0", 0, 0x7FFFFFFF, 0);
     t.ab_flags = (uint32_t)num("TSW_AB_FLAGS", 0, 255, t.ab_flags);
     t.t0_delay_us = (uint32_t)num("TSW_T0_DELAY_US", 0, 10000000, t.t0_delay_us);
     t.prefetch_ext = (uint32_t)num("TSW_PREFETCH_EXT", 0, 7, t.prefetch_ext);
@@ -1845,6 +1847,7 @@ int plan_impl(tsw_ctx* c, const tsw_point* starts, uint32_t n, const tsw_task* t
   init.unused = m;
   init.max_t = max_t;
   init.chase_id = c->chase_id;
+  init.move_rounds = c->tun.move_round0;
   tphase("plan dispatch starts");
   TRY(run_plan(c, P, init));
   tphase("plan dispatch done");
@@ -2160,6 +2163,7 @@ int tsw_step(tsw_ctx* c, uint32_t* v, uint32_t* g, uint32_t n) {
   PlanCtl init{};
   init.section = SEC_PRE1;
   init.chase_id = c->chase_id;
+  init.move_rounds = c->tun.move_round0;
   TRY(run_plan(c, P, init));
   HIPCHK(hipMemcpyAsync(v, c->d_v, n * 4ull, hipMemcpyDeviceToHost, c->s));
   HIPCHK(hipMemcpyAsync(g, c->d_g, n * 4ull, hipMemcpyDeviceToHost, c->s));

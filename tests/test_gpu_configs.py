@@ -64,6 +64,33 @@ def test_c3_full_horizon_matches_oracle(name):
     _plan_against_digests(name)
 
 
+def test_c3_busy_movement_round_tag_wrap():
+    """The movement rounds' MU words sit in LDS as u32 with a 16-bit round tag, cleared when the tag
+    wraps (tsw_plan.hip, MU32). Starting the round counter at 65,000 (TSW_MOVE_ROUND0, diagnostic
+    build) puts the wrap ~535 rounds into the busy C3 plan; every timestep must still match the oracle."""
+    import sys
+
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_digests import instances
+
+    name = "c3_busy_full"
+    ref, _ = _digests(name)
+    fac, max_t, _ = instances()[name]
+    rows, starts, tasks = fac()
+    old = os.environ.get("TSW_MOVE_ROUND0")
+    os.environ["TSW_MOVE_ROUND0"] = "65000"
+    try:
+        with Planner(rows, diag=True) as p:
+            rec, goals = p.plan_mapd_arrays(starts, tasks, max_t, trace_goals=True)
+            assert p.stats()["move_rounds"] > 65535
+    finally:
+        if old is None:
+            os.environ.pop("TSW_MOVE_ROUND0", None)
+        else:
+            os.environ["TSW_MOVE_ROUND0"] = old
+    _check_digests(name, rec, goals)
+
+
 @pytest.fixture(scope="module")
 def c5():
     rows, starts, tasks = maps.c5_instance()
