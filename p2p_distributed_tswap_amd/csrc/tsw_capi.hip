@@ -67,7 +67,7 @@ struct Tunables {
   bool prefetch = true;           // TSW_NO_PREFETCH: no speculative next-hop prefetch
   uint32_t wave_rules_max = 0xFFFFFFFFu;  // TSW_WAVE_RULES_MAX: wave-0 rules rounds when n <= this
   uint32_t wide_prefetch = 8;     // TSW_WIDE_PREFETCH: resolved hops walked ahead (0 = candidates only)
-  uint32_t wide_hi = 16, wide_lo = 4;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops with a small / large speculative backlog
+  uint32_t wide_hi = 32, wide_lo = 8;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops (grids <= 2^18 cells with a small backlog / grids > 2^18 cells); round 5, busy instances: 16 -> 32 and 4 -> 8 (profiles/r5/retune_busy_ab.txt)
   bool hot_chains = true;         // TSW_HOT_CHAINS=0: no planner-fed chains of just-assigned tasks (A/B)
   uint32_t chain_hops = 0;        // TSW_CHAIN_HOPS: hops resolved per task chain (0: the whole path)
   uint32_t move_round0 = 0;       // TSW_MOVE_ROUND0 (test knob): movement-round counter at the plan start (forces the MU32 tag wrap)

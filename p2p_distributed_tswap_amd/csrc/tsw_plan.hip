@@ -1325,10 +1325,12 @@ __global__ void __launch_bounds__(1024) k_plan(PlanArgs P, WorkerArgs Wk) {
       __syncthreads();
     } else if (sec == SEC_PRE1 || sec == SEC_PRE2) {
       if (sec == SEC_PRE1 && tid == 0) {
-        // walk-ahead depth (coop): 16 hops on grids up to 2^18 cells while the workers keep up with the
-        // speculative queue (8 when it backs up), 4 on larger grids, where every hop is a miss into a
-        // 1 MB-stride code store (round 4 A/Bs, profiles/r4/spec_depth_ab.txt: 16 hops wh10k 10.25 ->
-        // 9.68 s, C3 -1.6 %; C5 2.75 -> 3.16 s at 16 hops, 2.60 s at 4)
+        // walk-ahead depth (coop): wide_hi (32) hops on grids up to 2^18 cells while the workers keep up
+        // with the speculative queue (wide_prefetch, 8, when it backs up), wide_lo (8) on larger grids,
+        // where every hop is a miss into a 1 MB-stride code store. Round 4 set 16 / 4 on the frozen
+        // instances; round 5 re-measured on the busy ones (profiles/r5/retune_busy_ab.txt, the walk now
+        // resumes at its cached frontier): C3 0.98 -> 0.95 s, wh10k 11.66 -> 11.1-11.3 s at 32 hops
+        // (48: C3 slower), C5 7.74 -> 7.42 s at 8 hops (12 and 16 slower)
         uint32_t h = P.wide_prefetch ? P.wide_prefetch : 1u;
         if (P.coop && P.wide_prefetch && P.spec_hi) {
           if (P.ncell > (1u << 18)) {
