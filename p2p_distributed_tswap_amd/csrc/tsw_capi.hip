@@ -75,7 +75,7 @@ struct Tunables {
   uint32_t predict = 1;           // TSW_PREDICT: predicted task chains, bit 0 at pickups, bit 1 at delivery-goal changes (0: off)
   uint32_t urgent_hops = 1;       // TSW_URGENT_HOPS: walk-ahead pairs this close are queued as needed (0: off)
   uint32_t dag_width = 4;         // TSW_DAG_WIDTH: cells per DAG prefetch level (<= 16)
-  uint32_t dag_prefetch = 6;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (C3: 2 -> 6 levels, 465 -> 450 ms)
+  uint32_t dag_prefetch = 3;      // TSW_DAG_PREFETCH: DAG levels queued past the walk-ahead's first unresolved cell (round 2, frozen C3: 2 -> 6 levels, 465 -> 450 ms; round 5, busy instances with 32 / 8-hop walks: 3 best, profiles/r5/retune_busy_ab.txt)
   uint32_t prefetch_ext = 7;      // TSW_PREFETCH_EXT: bit 0 DAG from an agent's own unresolved cell, bit 1 walk past the pickup, bit 2 walk-ahead for agents a firing changed (C3 476 -> 409 ms with bits 0-1)
   bool flinks_lds = true;         // TSW_NO_FLINKS_LDS: pointer-doubling buffers stay global
   uint32_t part_lds = 0x7F;       // TSW_PART_LDS: PART_* agent arrays allowed in LDS one by one (tsw_plan.h)
