@@ -499,10 +499,10 @@ def main():
             # every table into its table store (sharding.py)
             from p2p_distributed_tswap_amd import sharding
 
-            build = lambda g, o: cp.dist_tables_device(g, o.data_ptr())  # noqa: E731
+            build_fn = lambda g, o: cp.dist_tables_device(g, o.data_ptr())  # noqa: E731
             barrier()
             tg = time.perf_counter()
-            full = sharding.build_and_allgather(goals, ncell, rank, world, build, dist, "cuda")
+            full = sharding.build_and_allgather(goals, ncell, rank, world, build_fn, dist, "cuda")
             barrier()
             gather_ms = allmax(time.perf_counter() - tg) * 1e3
             torch.cuda.synchronize()
