@@ -835,6 +835,18 @@ WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_
     c.lds = (size_t)h * 8u;
     c.waves = (uint32_t)num_cu * (uint32_t)std::min<size_t>(16u, WAVE_LDS_MAX / c.lds);
   }
+  // global g-score workers that keep the staged bitmap (wh10k's 112k cells: 14 KiB of bitmap): a 2,048-entry
+  // heap too when that raises the waves per CU by half or more — round 5, busy wh10k: 765 -> 1,275 workers,
+  // 11.07-11.13 -> 10.55 s, no query outgrowing the heap (profiles/r5/worker_cfg_ab.txt; round 4 measured
+  // it neutral on the frozen instance)
+  if (c.gs_lds == 0u && c.stage_fb != 0u && hcap_want == 0u && c.hcap > 2048u) {
+    WorkerCfg h2 = c;
+    const size_t rest = c.lds - (size_t)c.hcap * 8u;
+    h2.hcap = 2048u;
+    h2.lds = (size_t)h2.hcap * 8u + rest;
+    h2.waves = (uint32_t)num_cu * (uint32_t)std::min<size_t>(16u, WAVE_LDS_MAX / h2.lds);
+    if (2u * h2.waves >= 3u * c.waves) c = h2;
+  }
   // invariant the workers rely on (tsw_worker.h): LDS g-scores always come with the staged bitmap
   if (c.gs_lds != 0u) c.stage_fb = 1u;
   return c;
