@@ -143,7 +143,7 @@ struct Tunables {
     t.flinks_lds = getenv("TSW_NO_FLINKS_LDS") == nullptr;
     t.part_lds = (uint32_t)num("TSW_PART_LDS", 0, 0x7F, t.part_lds);
     t.occ_split = num("TSW_OCC_SPLIT", 0, 1, 1) != 0;
-    t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, 1024, 0) / 64u * 64u;
+    t.plan_block = (uint32_t)num("TSW_PLAN_BLOCK", 0, PLAN_BLOCK_MAX, 0) / 64u * 64u;
     t.plan_debug = getenv("TSW_PLAN_DEBUG") != nullptr;
     t.coop = num("TSW_COOP", 0, 1, 1) != 0;
     t.task_chains = num("TSW_TASK_CHAINS", 0, 1, 1) != 0;
@@ -1422,7 +1422,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
   // (they would compete for its SIMDs and LDS bandwidth on the critical path)
   if (P.coop) lds = std::max<size_t>(lds, (size_t)std::max(c->max_lds - 2048, 0));
   // one lane per agent in the parallel passes when possible; >= 4 waves for the task argmin
-  uint32_t block = std::min<uint32_t>(1024, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
+  uint32_t block = std::min<uint32_t>(PLAN_BLOCK_MAX, std::max<uint32_t>(256, (P.n + 63) / 64 * 64));
   if (c->tun.plan_block) block = std::max<uint32_t>(64u, c->tun.plan_block);
   WorkerArgs W{};
   uint32_t wblocks = 0;
@@ -2589,7 +2589,7 @@ int tsw_set_timing(tsw_ctx* c, int enabled) {
 int tsw_probe_round_floors(tsw_ctx* c, uint32_t block, double* out) {
   if (!c || !out) return TSW_EINVAL;
   NOT_FROM_RESOLVER(c);
-  if (block == 0) block = c->st.plan_block ? c->st.plan_block : 1024u;
+  if (block == 0) block = c->st.plan_block ? c->st.plan_block : PLAN_BLOCK_MAX;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->s));
   HIPCHK(probe_round_floors(block, std::max<uint32_t>(c->acap ? (uint32_t)c->acap : 1024u, 64u), c->s, &out[0],

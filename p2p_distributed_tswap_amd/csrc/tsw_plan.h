@@ -19,6 +19,10 @@ enum : uint32_t {
 };
 enum : uint32_t { PLAN_RUNNING = 0, PLAN_NEED_QUERIES = 1, PLAN_DONE = 2, PLAN_ERROR = 3 };
 enum : uint32_t { MODE_MAPD = 0, MODE_STEP = 1 };
+// k_plan's workgroup size cap (its __launch_bounds__). At 512 threads (2 waves per SIMD) a wave may use
+// 256 VGPRs: the planner's live state fits with no spill and no scratch; at 1,024 it was capped at 128
+// VGPRs with 67 spilled and 944 B of scratch per lane (round 6; scripts/isa_scratch.py).
+constexpr uint32_t PLAN_BLOCK_MAX = 512;
 constexpr uint32_t TASK_TAKEN = 0xFFFFFFFFu;  // PlanArgs::live entry of an assigned task
 
 // Persisted in device memory between launches (exact resume point).

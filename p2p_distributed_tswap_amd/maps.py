@@ -330,6 +330,14 @@ def wh10k_legacy_instance(n_agents: int = 10000, n_tasks: int = 30000, seed: int
     return rows, starts, tasks
 
 
+def c2_legacy_instance():
+    """Round 1-5 C2: 600 tasks drawn from all free cells (parking cells included); the plan spins to the
+    cap with only 180 of its 2,000 transitions moving an agent (VERDICT r5 missing #3)."""
+    rows = random_map(32, 32, 0.20, 0x3232)
+    starts, tasks = make_instance(rows, 200, 600, 0x3232)
+    return rows, starts, tasks
+
+
 def c3_legacy_instance():
     rows = warehouse_map(170, 84, 0x170084)
     starts, tasks = make_instance(rows, 1000, 3000, 0x170084)
@@ -339,7 +347,9 @@ def c3_legacy_instance():
 CONFIGS = {
     # name: (map factory, n_agents, n_tasks, instance seed)  — BASELINE.json configs
     "c1_bundled_10": (bundled_map, 10, 30, 1),
-    "c2_random_32_32_20": (lambda: random_map(32, 32, 0.20, 0x3232), 200, 600, 0x3232),
+    # well-formed (round 6), 16,000-task stream: ~10.2k assignments in 2,001 steps, every
+    # timestep moves agents (the round-1..5 600-task instance is c2_legacy_instance: 180 of 2,000 move)
+    "c2_random_32_32_20": (lambda: random_map(32, 32, 0.20, 0x3232), 200, 16000, 0x3232),
     # well-formed, 32,000-task stream: ~24k deliveries in 2,001 steps, every timestep moves agents
     "c3_warehouse_170x84": (lambda: warehouse_map(170, 84, 0x170084), 1000, 32000, 0x170084),
     # K1-only config: 10,000 distinct goal cells (BFS tables), goal-sharded over 2/4/8 GPUs
@@ -348,7 +358,7 @@ CONFIGS = {
     "c5_sortation_1024_10k": (lambda: sortation_map(1024, 1024), 10000, 24000, 0x1024),
 }
 # configs whose instance is well-formed (make_wf_instance)
-WELL_FORMED = {"c3_warehouse_170x84", "c5_sortation_1024_10k"}
+WELL_FORMED = {"c2_random_32_32_20", "c3_warehouse_170x84", "c5_sortation_1024_10k"}
 # distinct K1 goals of the table-build configs
 CONFIG_GOALS = {"c4_den520d_10k_goals": 10000, "c5_sortation_1024_10k": 10000}
 

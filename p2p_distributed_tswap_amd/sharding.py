@@ -140,12 +140,16 @@ class ShardedK3:
         pairs = np.concatenate([start, goal]).astype(np.int32) if self.rank == 0 else None
         pairs = self._bcast(pairs, torch.int32, 2 * k).astype(np.uint32)
         st, gl = pairs[:k], pairs[k:]
-        try:
-            mine = _codes_for_rank(st, gl, self.rank, self.world, self.codes_fn).astype(np.int32)
-        except Exception as e:  # noqa: BLE001 — reported after the collective, on every rank
-            if self.local_error is None:
-                self.local_error = e
+        if self.local_error is not None:
+            # this rank already failed once (possibly a broken HIP context): do not re-enter codes_fn for
+            # the rest of the plan, contribute FAILED until rank 0 sends finish()
             mine = np.full(k, self.FAILED, dtype=np.int32)
+        else:
+            try:
+                mine = _codes_for_rank(st, gl, self.rank, self.world, self.codes_fn).astype(np.int32)
+            except Exception as e:  # noqa: BLE001 — reported after the collective, on every rank
+                self.local_error = e
+                mine = np.full(k, self.FAILED, dtype=np.int32)
         # u8 codes ride in an int32 tensor (MIN over ranks: the owner's code, others 0xFF; FAILED wins)
         t = torch.from_numpy(mine).to(self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)

@@ -64,6 +64,13 @@ def test_c3_full_horizon_matches_oracle(name):
     _plan_against_digests(name)
 
 
+@pytest.mark.parametrize("name", ["c2_busy_full", "c2_legacy_full"])
+def test_c2_full_horizon_matches_oracle(name):
+    """C2 (configs[1], random-32-32-20, 200 agents) over the full horizon: the well-formed 16,000-task
+    stream (every transition moves agents; round 6, VERDICT r5 #4) and the round-1..5 600-task instance."""
+    _plan_against_digests(name)
+
+
 def test_c3_busy_movement_round_tag_wrap():
     """The movement rounds' MU words sit in LDS as u32 with a 16-bit round tag, cleared when the tag
     wraps (tsw_plan.hip, MU32). Starting the round counter at 65,000 (TSW_MOVE_ROUND0, diagnostic

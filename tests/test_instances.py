@@ -49,7 +49,7 @@ def test_wf_instance_window():
     assert not (_cells(starts) & (_cells(tasks[:, :2]) | _cells(tasks[:, 2:])))
 
 
-@pytest.mark.parametrize("name", ["c3_warehouse_170x84", "c5_sortation_1024_10k"])
+@pytest.mark.parametrize("name", ["c2_random_32_32_20", "c3_warehouse_170x84", "c5_sortation_1024_10k"])
 def test_bench_configs_are_well_formed(name):
     rows, starts, tasks = maps.config_instance(name)
     _, n, m, _ = maps.CONFIGS[name]
@@ -57,7 +57,7 @@ def test_bench_configs_are_well_formed(name):
     assert not (_cells(starts) & (_cells(tasks[:, :2]) | _cells(tasks[:, 2:])))
 
 
-@pytest.mark.parametrize("name", ["c3_busy_full", "wh10k_busy_full", "c5_busy_full"])
+@pytest.mark.parametrize("name", ["c2_busy_full", "c3_busy_full", "wh10k_busy_full", "c5_busy_full"])
 def test_busy_digests_change_at_every_timestep(name):
     """Done-criterion of VERDICT r4 #1: the committed full-horizon digests of the busy instances change
     at >= 95 % of timesteps (the plan runs to the cap with agents moving)."""
@@ -76,3 +76,14 @@ def test_legacy_digests_freeze(name, frozen_from):
     dig = load(name)["digests"]
     assert len(set(dig[frozen_from:])) == 1
     assert dig[frozen_from - 1] != dig[frozen_from] or dig[frozen_from - 2] != dig[frozen_from - 1]
+
+
+def test_c2_busy_moves_at_every_transition():
+    """C2 (configs[1]) planned by the oracle moves agents at all 2,000 transitions with the
+    well-formed 16,000-task stream, where the legacy 600-task instance moved at 180 of them."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+    from oracle import OracleGraph
+
+    rows, starts, tasks = maps.config_instance("c2_random_32_32_20")
+    rec, _ = OracleGraph(maps.rows_to_array(rows)).mapd(starts, tasks, 300, trace_goals=True)
+    assert rec.shape == (200, 301) and maps.moving_timesteps(rec) == 300
