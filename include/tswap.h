@@ -63,7 +63,7 @@ extern "C" {
  * tsw_next_hop_tables_device gained dev_dist; 4: tsw_abi_version, lazy task-cell checks,
  * tsw_plan_mapd_resolved / tsw_next_hop_codes; 5: tsw_build_id, entry points refuse re-entry from a
  * tsw_plan_mapd_resolved resolver (TSW_EINVAL). */
-#define TSW_ABI_VERSION 5
+#define TSW_ABI_VERSION 6
 
 /* AgentState discriminants in declaration order (src/map/agent.rs:9-15) */
 #define TSW_PICKING 0
@@ -285,6 +285,10 @@ typedef struct {
     double coop_worker_busy_ms[3];
     uint64_t watchdog_fires;    /* plan calls the host watchdog moved to exit mode */
     uint64_t tableless_goals;   /* goals held without a distance table (u16 overflow; next hops by K3) */
+    /* coop mode (ABI 6): A* queries the workers ran and the heap pops they took, by queue (as
+     * coop_worker_busy_ms): busy / pops = the in-dispatch time per pop */
+    uint64_t coop_worker_queries[3];
+    uint64_t coop_worker_pops[3];
 } tsw_stats;
 int tsw_get_stats(const tsw_ctx *ctx, tsw_stats *out);
 int tsw_reset_stats(tsw_ctx *ctx);

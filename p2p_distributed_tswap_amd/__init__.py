@@ -35,7 +35,7 @@ LIB_PATH = os.path.join(_HERE, "libtswap_hip.so")
 DIAG_LIB_PATH = os.path.join(_HERE, "libtswap_hip_diag.so")
 
 TSW_OK, TSW_EINVAL, TSW_ENOMEM, TSW_EHIP, TSW_EOVERFLOW = 0, -22, -12, -5, -75
-TSW_ABI_VERSION = 5  # include/tswap.h
+TSW_ABI_VERSION = 6  # include/tswap.h
 TSW_F_EAGER_NEXTHOP, TSW_F_LAZY_NEXTHOP, TSW_F_EXIT_MODE = 1, 2, 4
 # TswapAction (bin/decentralized/agent.rs:321-326), include/tswap.h TSW_ACT_*
 TSW_ACT_MOVE, TSW_ACT_GOAL_SWAP, TSW_ACT_ROTATION, TSW_ACT_WAIT = 0, 1, 2, 3
@@ -99,6 +99,7 @@ class Stats(ctypes.Structure):
         ("move_rounds", ctypes.c_uint64), ("plan_block", ctypes.c_uint32),
         ("coop_workers", ctypes.c_uint32), ("coop_worker_busy_ms", ctypes.c_double * 3),
         ("watchdog_fires", ctypes.c_uint64), ("tableless_goals", ctypes.c_uint64),
+        ("coop_worker_queries", ctypes.c_uint64 * 3), ("coop_worker_pops", ctypes.c_uint64 * 3),
     ]
 
     def as_dict(self):
@@ -108,6 +109,8 @@ class Stats(ctypes.Structure):
         d["coop_wait_sec_ms"] = list(self.coop_wait_sec_ms)
         d["coop_waits_sec"] = list(self.coop_waits_sec)
         d["coop_worker_busy_ms"] = list(self.coop_worker_busy_ms)
+        d["coop_worker_queries"] = list(self.coop_worker_queries)
+        d["coop_worker_pops"] = list(self.coop_worker_pops)
         return d
 
 

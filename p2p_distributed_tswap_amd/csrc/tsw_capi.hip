@@ -1557,7 +1557,11 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       }
       c->st.astar_queries += cc.worker_queries;
       c->st.coop_workers = W.nworkers;
-      for (int k = 0; k < 3; ++k) c->st.coop_worker_busy_ms[k] += (double)cc.wbusy[k] / (double)c->wall_khz;
+      for (int k = 0; k < 3; ++k) {
+        c->st.coop_worker_busy_ms[k] += (double)cc.wbusy[k] / (double)c->wall_khz;
+        c->st.coop_worker_queries[k] += cc.wcount[k];
+        c->st.coop_worker_pops[k] += cc.wpops[k];
+      }
       if (cc.err) RET(TSW_EOVERFLOW, "K3 worker: A* heap overflow");
       // speculative pairs nobody claimed stay PENDING_S: back to UNKNOWN for later calls — only the
       // unclaimed queue entries (every claimed one was resolved, or reset by the worker that dropped
@@ -1570,6 +1574,14 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     }
     const PlanCtl& k = *c->h_ctl;
     if (k.err & ERR_ABORT) {
+      if (c->tun.plan_debug) {  // diagnostics: where the stopped planner spent its time (section / sub-phase ticks)
+        unsigned long long tk[40];
+        if (hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost) == hipSuccess) {
+          std::string line = "[k_plan] watchdog stop, ticks:";
+          for (int q = 0; q < 40; ++q) line += " " + std::to_string(q) + ":" + std::to_string(tk[q]);
+          fprintf(stderr, "%s\n", line.c_str());
+        }
+      }
       char buf[256];
       snprintf(buf, sizeof buf,
                "planner stopped by the watchdog (no timestep for %u ms): t %u section %u cursor %u, %u rule rounds, "

@@ -37,6 +37,16 @@
 #include "tsw_plan.h"
 #include "tsw_worker.h"
 
+// Planner instrumentation (TSW_PLAN_DEBUG: sub-phase ticks, change tags, wait classes) exists in the
+// diagnostic build only: the product kernel carries none of it (round 6 — with every helper inlined, the
+// diagnostic build's planner hangs in its first rules phase as soon as any instrumentation branch
+// executes, scripts/inline_bisect.sh and DESIGN.md; the product never executes them and passes).
+#ifdef TSW_DIAG
+#define PLAN_DBG (P.dbg != 0u)
+#else
+#define PLAN_DBG false
+#endif
+
 namespace tsw {
 
 namespace {
@@ -363,7 +373,7 @@ __device__ __forceinline__ uint32_t refresh_codes(const PlanArgs& P, const Array
     if (code <= NH_STAY) {
       S.NHC[k] = code;
     } else {
-      if (P.dbg && P.coop && (code == NH_UNKNOWN || code == NH_PENDING_S)) {
+      if (PLAN_DBG && P.coop && (code == NH_UNKNOWN || code == NH_PENDING_S)) {
         const uint32_t grp = sec == SEC_PRE1 ? 0u : sec == SEC_RULES ? 1u : 2u;
         atomicAdd(&P.cc->dbg_need[2u * grp + (code == NH_PENDING_S ? 1u : 0u)], 1u);
         // PRE1, never queued: assigned a task / picked up in this step's ASSIGN (DEC tag, diagnostics)
@@ -445,7 +455,7 @@ __device__ __forceinline__ int coop_wait(const PlanArgs& P, const Arrays& S, uin
   if (tid == 0) {
     coop_publish(P, s_q);
     *s_flag = COOP_OK;
-    if (P.dbg) {
+    if (PLAN_DBG) {
       const uint32_t hs = min(s_q[1], P.qscap), cs = ld_agent(&P.cc->claim_s);
       const uint32_t dep = hs > cs ? hs - cs : 0u;
       P.cc->dbg_depth += dep;
@@ -494,7 +504,7 @@ __device__ __forceinline__ int coop_wait(const PlanArgs& P, const Arrays& S, uin
     // pickup arrivals, 7: neither — walking agents)
     {
       const uint32_t kslot[6] = {0u, 0u, 3u, 5u, 6u, 7u};
-      sec = (P.dbg && (sec >> 8)) ? kslot[sec >> 8] : min(sec & 0xFFu, 7u);
+      sec = (PLAN_DBG && (sec >> 8)) ? kslot[sec >> 8] : min(sec & 0xFFu, 7u);
     }
     P.cc->waits += 1u;
     P.cc->wait_ticks += dt;
@@ -770,52 +780,81 @@ __device__ __forceinline__ void nextnext_prefetch(const PlanArgs& P, const Array
 }
 
 // Serial movement phase (tswap.rs:257-285) — used when cells are shared by several agents
-// (duplicate start cells); false on an unresolved next hop.
-__device__ __forceinline__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
-  const uint32_t n = P.n, W = P.W;
-  uint32_t i = ctl.i;
+// (duplicate start cells). Scans agents from i0; returns the agent it stopped at (n when done) and sets
+// *miss to 1 on an unresolved next hop, 2 on a goal without a table. Kept out of line, with its inputs
+// by value (no reference to PlanArgs / Arrays / the LDS control block escapes, so the kernel keeps
+// PlanArgs in its kernel-argument registers): with this cold path inlined, the diagnostic build's planner
+// hung in the first rules phase of every plan (round 6, scripts/inline_bisect.sh).
+__device__ __attribute__((noinline)) uint32_t walk_move(uint32_t n, uint32_t W, const uint8_t* nh, uint64_t nstride,
+                                                        uint32_t coop, uint32_t* V, const uint32_t* G, uint8_t* NHC,
+                                                        const int32_t* GT, uint32_t* OCC, uint32_t i0, uint32_t* miss) {
+  auto code_of = [&](uint32_t k) -> int {  // lookup_code
+    const uint8_t c = NHC[k];
+    if (c <= NH_STAY) return c;
+    const int32_t tab = GT[k];
+    if (tab < 0) return -2;
+    const uint8_t* p = nh + (uint64_t)tab * nstride + V[k];
+    uint8_t code = *p;
+    if (coop && (code == NH_PENDING || code == NH_PENDING_S)) {  // nh_code's agent-scope re-read
+      const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      code = (uint8_t)(w >> (8u * (uint32_t)((uintptr_t)p & 3u)));
+    }
+    if (code <= NH_STAY) {
+      NHC[k] = code;
+      return code;
+    }
+    return -1;
+  };
+  auto rescan = [&](uint32_t cell) {  // occ_rescan
+    uint32_t lowest = OCC_NONE, cnt = 0;
+    for (uint32_t k = 0; k < n; ++k)
+      if (V[k] == cell) {
+        if (cnt == 0) lowest = k;
+        ++cnt;
+      }
+    OCC[cell] = cnt == 0 ? OCC_NONE : (lowest | (cnt > 1 ? OCC_FLAG : 0u));
+  };
+  uint32_t i = i0;
   for (; i < n; ++i) {
-    const uint32_t vi = S.V[i], gi = S.G[i];
+    const uint32_t vi = V[i], gi = G[i];
     if (vi == gi) continue;
-    const int code = lookup_code(P, S, i);
+    const int code = code_of(i);
     if (code < 0) {
-      ctl.miss = code == -2 ? 2u : 1u;
-      ctl.i = i;
-      return false;
+      *miss = code == -2 ? 2u : 1u;
+      return i;
     }
     const uint32_t u = step_cell(vi, (uint32_t)code, W);
-    const uint32_t o = S.OCC[u];
+    const uint32_t o = OCC[u];
     if (o == OCC_NONE) {  // rule 2: move
-      S.V[i] = u;
-      S.NHC[i] = NHC_DIRTY;
-      S.OCC[u] = i;
-      if (S.OCC[vi] & OCC_FLAG) occ_rescan(P, S, vi);
-      else S.OCC[vi] = OCC_NONE;
+      V[i] = u;
+      NHC[i] = NHC_DIRTY;
+      OCC[u] = i;
+      if (OCC[vi] & OCC_FLAG) rescan(vi);
+      else OCC[vi] = OCC_NONE;
     } else if ((o & OCC_IDX) != i) {
       const uint32_t j = o & OCC_IDX;
-      const uint32_t vj = S.V[j], gj = S.G[j];
+      const uint32_t vj = V[j], gj = G[j];
       if (vj != gj) {
-        const int cj = lookup_code(P, S, j);
+        const int cj = code_of(j);
         if (cj < 0) {
-          ctl.miss = cj == -2 ? 2u : 1u;
-          ctl.i = i;
-          return false;
+          *miss = cj == -2 ? 2u : 1u;
+          return i;
         }
         if (step_cell(vj, (uint32_t)cj, W) == vi) {  // mutual swap (:273-278)
-          S.V[i] = vj;
-          S.V[j] = vi;
-          S.NHC[i] = NHC_DIRTY;
-          S.NHC[j] = NHC_DIRTY;
-          if (S.OCC[vi] & OCC_FLAG) occ_rescan(P, S, vi);
-          else S.OCC[vi] = j;
-          if (o & OCC_FLAG) occ_rescan(P, S, vj);
-          else S.OCC[vj] = i;
+          V[i] = vj;
+          V[j] = vi;
+          NHC[i] = NHC_DIRTY;
+          NHC[j] = NHC_DIRTY;
+          if (OCC[vi] & OCC_FLAG) rescan(vi);
+          else OCC[vi] = j;
+          if (o & OCC_FLAG) rescan(vj);
+          else OCC[vj] = i;
         }
       }
     }
   }
-  ctl.i = n;
-  return true;
+  return n;
 }
 
 }  // namespace
@@ -823,12 +862,12 @@ __device__ __forceinline__ bool walk_move(const PlanArgs& P, const Arrays& S, Pl
 // diagnostics: wall-clock ticks of sub-phases (P.sec_ticks[8..15], printed by TSW_PLAN_DEBUG)
 #define DTAG(k, bits)                                        \
   do {                                                       \
-    if (P.dbg && P.dtag) atomicOr(&P.dtag[(k)], (uint32_t)(bits)); \
+    if (PLAN_DBG && P.dtag) atomicOr(&P.dtag[(k)], (uint32_t)(bits)); \
   } while (0)
 
 #define PLAN_TICK(slot)                              \
   do {                                               \
-    if (P.dbg && tid == 0) {                         \
+    if (PLAN_DBG && tid == 0) {                         \
       const unsigned long long nw_ = wall_clock64(); \
       s_tick[slot] += nw_ - s_tp;                    \
       s_tp = nw_;                                    \
@@ -1056,7 +1095,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
       // agents below it still happen (and may panic first, :136), none above it.
       if (tid == 0) {
         s_nassign = s_npick = s_bad = 0;
-        if (P.dbg) {
+        if (PLAN_DBG) {
           s_tp = wall_clock64();
           s_tick[39] += 1;  // diagnostics: ASSIGN sections (sub-phase ticks in [32..38])
         }
@@ -1073,7 +1112,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
             if (st == ST_TO_PICKUP) {
               st = ST_TO_DELIVERY;
               atomicAdd(&s_npick, 1u);
-              if (P.dbg) S.DEC[i] = 0x41;  // diagnostics tag (MOVE re-initialises DEC)
+              if (PLAN_DBG) S.DEC[i] = 0x41;  // diagnostics tag (MOVE re-initialises DEC)
               DTAG(i, 32u);
               const int32_t tk = P.task[i];
               if (tk >= 0) {
@@ -1256,7 +1295,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
             s_cnt2 = acc;
             s_doit = stop;
             s_nassign += acc;
-            if (P.dbg) {
+            if (PLAN_DBG) {
               s_tick[37] += 1;    // batches
               s_tick[38] += acc;  // agents accepted
             }
@@ -1278,7 +1317,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
               else if (pt == 0xFFFFFFFFu) atomicAdd(&P.cc->pred_none, 1u);
               __hip_atomic_store(&P.pred[ai], 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (P.dbg) S.DEC[ai] = 0x40;
+            if (PLAN_DBG) S.DEC[ai] = 0x40;
             DTAG(ai, 16u);
             const uint32_t ng = P.pick[t];
             if (ng == CELL_BAD) {  // pos2id[&task.pickup] panics (tswap.rs:136)
@@ -1363,7 +1402,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
         s_hops = h;
       }
       const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
-      if (P.dbg && P.dtag && P.coop && sec == SEC_PRE1) {  // diagnostics: unresolved PRE1 pairs by agent tag
+      if (PLAN_DBG && P.dtag && P.coop && sec == SEC_PRE1) {  // diagnostics: unresolved PRE1 pairs by agent tag
         for (uint32_t k = tid; k < n; k += bd) {
           const uint32_t tg = P.dtag[k] & 63u;
           P.dtag[k] = 0u;
@@ -1381,9 +1420,9 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
       // the assignment exit's K3 batch (if any) already carries what the movement phase reads
       if (sec == SEC_PRE1 && P.prefetch) nextnext_prefetch(P, S, s_q, s_hops);
       if (P.coop && tid == 0) {  // speculative pairs start resolving now
-        const unsigned long long t0 = P.dbg ? wall_clock64() : 0ull;
+        const unsigned long long t0 = PLAN_DBG ? wall_clock64() : 0ull;
         coop_publish(P, s_q);
-        if (P.dbg) {
+        if (PLAN_DBG) {
           s_tick[24] += wall_clock64() - t0;
           s_tick[25] += 1;
         }
@@ -1413,24 +1452,24 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
       // s — terminal until now — gains one out-edge, so the only new cycle possible is
       // one through s. CANDC[k] prefetches s's next hop toward k's goal for every rule-3
       // candidate k, so a swap needs no global round trip on the serial path.
-      if (P.dbg && tid == 0) s_tp = wall_clock64();
+      if (PLAN_DBG && tid == 0) s_tp = wall_clock64();
       const bool fuse_pf = P.prefetch && P.wide_prefetch;  // rules_prefetch inside the first pass
       rules_init(P, S, fuse_pf ? s_q : nullptr);
       if (tid == 0) s_ctl.relabel_full += 1;
-      if (P.dbg && tid == 0) {
+      if (PLAN_DBG && tid == 0) {
         const unsigned long long nw = wall_clock64();
         s_tick[26] += nw - s_tp;
         s_tp = nw;
       }
       if (P.prefetch && !fuse_pf) rules_prefetch(P, S, s_q);
-      if (P.dbg && tid == 0) {
+      if (PLAN_DBG && tid == 0) {
         const unsigned long long nw = wall_clock64();
         s_tick[27] += nw - s_tp;
         s_tp = nw;
       }
       if (P.coop && tid == 0) {
         coop_publish(P, s_q);
-        if (P.dbg) {
+        if (PLAN_DBG) {
           s_tick[28] += wall_clock64() - s_tp;
           s_tick[29] += 1;
         }
@@ -1509,7 +1548,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
                 }
                 x = nx;
               }
-              if (P.dbg) s_tick[9] += it;  // diagnostics: rule-3 cycle-walk hops
+              if (PLAN_DBG) s_tick[9] += it;  // diagnostics: rule-3 cycle-walk hops
               if (x == s) {
                 uint32_t y = s;
                 do {
@@ -1554,7 +1593,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
             note_changed(ap[kk]);
             DTAG(ap[kk], 4u);
           }
-          if (P.dbg) s_tick[11] += 1;  // diagnostics: rule-4 rotations
+          if (PLAN_DBG) s_tick[11] += 1;  // diagnostics: rule-4 rotations
         }
         s_ctl.i = b + 1;
         s_ctl.rule_rounds += 1;
@@ -1597,7 +1636,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
             // exactly the new cycles; their members label them. Same labels as relabel_walks.
             wave_order();
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the code stores above are visible
-            const unsigned long long rt0 = P.dbg ? clock64() : 0ull;
+            const unsigned long long rt0 = PLAN_DBG ? clock64() : 0ull;
             uint8_t cc = NHC_DIRTY;
             uint32_t a = 0;
             const bool mem = lane < L;
@@ -1611,7 +1650,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
             }
             wave_order();
             __builtin_amdgcn_s_waitcnt(0xC07F);
-            const unsigned long long rt1 = P.dbg ? clock64() : 0ull;
+            const unsigned long long rt1 = PLAN_DBG ? clock64() : 0ull;
             uint32_t nm = 64u;  // next member's index (64: the walk ended without one)
             bool fail = false;
             if (mem) {
@@ -1654,7 +1693,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
             if (mem) S.CANDC[a] = cc;
             wave_order();
             ok = __ballot(fail) ? 0u : 1u;
-            if (P.dbg && lane == 0) {  // diagnostics: rotation settle split (successors | walks)
+            if (PLAN_DBG && lane == 0) {  // diagnostics: rotation settle split (successors | walks)
               const unsigned long long rt2 = clock64();
               s_tick[30] += rt1 - rt0;
               s_tick[31] += rt2 - rt1;
@@ -1746,9 +1785,9 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
               pv = ok;
             };
             // diagnostics (TSW_PLAN_DEBUG): shader cycles per part of the loop -> s_tick[16..23]
-            unsigned long long pt = P.dbg ? clock64() : 0ull;
+            unsigned long long pt = PLAN_DBG ? clock64() : 0ull;
             auto prof = [&](int slot) {
-              if (P.dbg) {
+              if (PLAN_DBG) {
                 const unsigned long long nw = clock64();
                 if (lane == 0) s_tick[slot] += nw - pt;
                 pt = nw;
@@ -1784,7 +1823,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
                 m = __ballot(f);
                 precompute(f);
                 loaded = true;
-                if (P.dbg && lane == 0) s_tick[22] += 1;
+                if (PLAN_DBG && lane == 0) s_tick[22] += 1;
                 prof(16);
               }
               if (!m) {
@@ -1869,7 +1908,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
                   s_ctl.i = k + 1u;
                 }
                 m = last == 63u ? 0ull : (__ballot(f) & ~((2ull << last) - 1ull));
-                if (P.dbg && lane == 0) s_tick[23] += nb;
+                if (PLAN_DBG && lane == 0) s_tick[23] += nb;
                 prof(18);
                 continue;
               }
@@ -1897,7 +1936,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
                     S.SUCC[b] = p_nk;
                     S.ONC[b] = 0;
                     S.ONC[s] = 0;
-                    if (P.dbg) s_tick[11] += 1;  // diagnostics: rule-4 rotations
+                    if (PLAN_DBG) s_tick[11] += 1;  // diagnostics: rule-4 rotations
                   }
                   s_best = b;
                   s_miss = 0;
@@ -1921,7 +1960,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
                       }
                       x = nx;
                     }
-                    if (P.dbg) s_tick[9] += it;
+                    if (PLAN_DBG) s_tick[9] += it;
                     if (x == st) {
                       uint32_t y = st;
                       do {
@@ -1998,7 +2037,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
                         s_miss = 0;
                         s_ctl.i = b + 1;
                         s_ctl.rule_rounds += 1;
-                        if (P.dbg) s_tick[11] += 1;  // diagnostics: rule-4 rotations
+                        if (PLAN_DBG) s_tick[11] += 1;  // diagnostics: rule-4 rotations
                       }
                       r_fl = FO_ROT | FO_WAVE;
                       r_ns = L;
@@ -2156,12 +2195,16 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
       __syncthreads();
     } else if (sec == SEC_MOVE && P.has_dups) {
       if (tid == 0) {
-        s_ctl.miss = 0;
-        if (walk_move(P, S, s_ctl)) {
+        uint32_t miss = 0;
+        const uint32_t at = walk_move(n, W, P.nh, P.nstride, P.coop, S.V, S.G, S.NHC, S.GT, S.OCC, s_ctl.i, &miss);
+        s_ctl.miss = miss;
+        if (miss == 0u) {
           s_ctl.section = SEC_RECORD;
           s_ctl.i = 0;
+        } else {
+          s_ctl.i = at;
         }
-        if (s_ctl.miss == 2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
+        if (miss == 2u) atomicOr(&P.ctl->err, ERR_NO_TABLE);
       }
       __syncthreads();
       if (s_ctl.miss) {
@@ -2304,7 +2347,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
           s_miss = 0;
           s_best = NO_AGENT;
           s_ctl.move_rounds += 1;
-          if (P.dbg) s_tp = wall_clock64();
+          if (PLAN_DBG) s_tp = wall_clock64();
           if ((s_ctl.move_rounds & 1023u) == 0u && plan_abort(P)) s_abort = 1;
         }
         __syncthreads();

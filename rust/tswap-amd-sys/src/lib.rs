@@ -35,7 +35,7 @@ pub const TSW_ENODEV: c_int = -19;
 
 /// ABI revision of include/tswap.h this crate mirrors; `Planner::new` refuses a library built
 /// against another one.
-pub const TSW_ABI_VERSION: c_int = 5;
+pub const TSW_ABI_VERSION: c_int = 6;
 
 pub const TSW_PICKING: u8 = 0;
 pub const TSW_CARRYING: u8 = 1;
@@ -128,6 +128,8 @@ pub struct TswStats {
     pub coop_worker_busy_ms: [f64; 3],
     pub watchdog_fires: u64,
     pub tableless_goals: u64,
+    pub coop_worker_queries: [u64; 3],
+    pub coop_worker_pops: [u64; 3],
 }
 
 extern "C" {

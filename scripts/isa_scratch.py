@@ -66,3 +66,35 @@ if __name__ == "__main__":
     print("-- SGPR-spill lane moves by source line")
     for k, v in r["lanes_by_line"]:
         print(f"  {k:28s} {v}")
+
+
+def per_line_mix(path: str, fn: str, src: str, lo: int, hi: int) -> dict:
+    """Static instruction mix (valu / salu / ds / vmem / lane moves) per source line of `src` in [lo, hi]
+    for the function matching `fn` (a loop body's cost model: which lines carry the instructions)."""
+    files: dict[int, str] = {}
+    lines = open(path).read().split("\n")
+    start = None
+    for i, l in enumerate(lines):
+        m = re.match(r"\s*\.file\s+(\d+)\s+\"[^\"]*\"\s+\"([^\"]+)\"", l)
+        if m:
+            files[int(m.group(1))] = m.group(2)
+        if start is None and re.match(r"^_Z\w*" + re.escape(fn) + r"\w*:", l):
+            start = i
+    per: dict[int, collections.Counter] = collections.defaultdict(collections.Counter)
+    loc = None
+    for l in lines[start + 1:]:
+        s = l.strip()
+        if s.startswith(".Lfunc_end"):
+            break
+        m = re.match(r"\.loc\s+(\d+)\s+(\d+)", s)
+        if m:
+            f = files.get(int(m.group(1)), "")
+            loc = int(m.group(2)) if f.endswith(src) else None
+            continue
+        if loc is None or not (lo <= loc <= hi) or not s or s[0] in ".;" or s.endswith(":"):
+            continue
+        op = s.split()[0]
+        cat = ("lane" if op.startswith(("v_readlane", "v_writelane", "v_readfirstlane")) else "valu" if op.startswith("v_")
+               else "salu" if op.startswith("s_") else "ds" if op.startswith("ds_") else "vmem")
+        per[loc][cat] += 1
+    return {k: dict(v) for k, v in sorted(per.items())}
