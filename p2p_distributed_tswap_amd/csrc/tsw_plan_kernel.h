@@ -37,15 +37,12 @@
 #include "tsw_plan.h"
 #include "tsw_worker.h"
 
-// Planner instrumentation (TSW_PLAN_DEBUG: sub-phase ticks, change tags, wait classes) exists in the
-// diagnostic build only: the product kernel carries none of it (round 6 — with every helper inlined, the
-// diagnostic build's planner hangs in its first rules phase as soon as any instrumentation branch
-// executes, scripts/inline_bisect.sh and DESIGN.md; the product never executes them and passes).
-#ifdef TSW_DIAG
+// Planner instrumentation (TSW_PLAN_DEBUG, diagnostic build: sub-phase ticks, change tags, wait classes).
+// Round 6 note: the helpers below stay out of line (as in rounds 1-5). Force-inlining them all took
+// PlanArgs off the stack (0 B scratch) but the fully inlined planner hung in its first rules phase
+// whenever an instrumentation branch ran, and in a two-process run without them;
+// scripts/exp_lib.sh + hang_probe.py reproduce it.
 #define PLAN_DBG (P.dbg != 0u)
-#else
-#define PLAN_DBG false
-#endif
 
 namespace tsw {
 
@@ -138,7 +135,7 @@ __device__ __forceinline__ int lookup_code(const PlanArgs& P, const Arrays& S, u
   return -1;
 }
 
-__device__ __forceinline__ void occ_rescan(const PlanArgs& P, const Arrays& S, uint32_t cell) {
+__device__ void occ_rescan(const PlanArgs& P, const Arrays& S, uint32_t cell) {
   uint32_t lowest = OCC_NONE, cnt = 0;
   for (uint32_t k = 0; k < P.n; ++k)
     if (S.V[k] == cell) {
@@ -169,7 +166,7 @@ __device__ __forceinline__ uint32_t succ_of(const PlanArgs& P, const Arrays& S, 
 // separate block-wide pass and its repeated table reads.
 __device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uint32_t g, int32_t tab, uint32_t* s_q);
 __device__ __forceinline__ bool spec_full(const PlanArgs& P, const uint32_t* s_q);
-__device__ __forceinline__ void rules_init(const PlanArgs& P, const Arrays& S, uint32_t* pf = nullptr) {
+__device__ void rules_init(const PlanArgs& P, const Arrays& S, uint32_t* pf = nullptr) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x, n = P.n;
   for (uint32_t k = tid; k < n; k += bd) {
     const uint32_t s = succ_of(P, S, k);
@@ -233,15 +230,15 @@ __device__ __forceinline__ void relabel_reset(const PlanArgs& P, const Arrays& S
 }
 
 // the walks of rules_relabel_changed, after relabel_reset of every agent in lst
-__device__ __forceinline__ bool relabel_walks(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt, uint32_t limit);
+__device__ bool relabel_walks(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt, uint32_t limit);
 
-__device__ __forceinline__ bool rules_relabel_changed(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt,
+__device__ bool rules_relabel_changed(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt,
                                       uint32_t limit) {
   for (uint32_t i = 0; i < cnt; ++i) relabel_reset(P, S, lst[i]);
   return relabel_walks(P, S, lst, cnt, limit);
 }
 
-__device__ __forceinline__ bool relabel_walks(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt, uint32_t limit) {
+__device__ bool relabel_walks(const PlanArgs& P, const Arrays& S, const uint32_t* lst, uint32_t cnt, uint32_t limit) {
   for (uint32_t i = 0; i < cnt; ++i) {
     const uint32_t a = lst[i];
     if (S.ONC[a]) continue;  // labelled by an earlier walk of this loop
@@ -355,7 +352,7 @@ __device__ __forceinline__ void prefetch_pair(const PlanArgs& P, uint32_t v, uin
 // appended to the launch's K3 queue (s_q counts every pair queued since the launch began,
 // speculative prefetches included). Returns how many dirty agents still lack a code
 // (block-uniform): the planner must exit for K3 iff that is nonzero.
-__device__ __forceinline__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need,
+__device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need,
                                   uint32_t sec) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   if (tid == 0) *s_need = 0;
@@ -450,7 +447,7 @@ enum : int { COOP_OK = 0, COOP_GIVE_UP = 1, COOP_RETRY = 2 };
 // safety limit (the caller exits to the host). COOP_RETRY: a pair stayed pending for 20 ms — more
 // than any A* on these grids; the caller queues the still-pending pairs again (a duplicate query
 // resolves to the same code), so a lost update can cost a retry but never a stall.
-__device__ __forceinline__ int coop_wait(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_flag, uint32_t sec) {
+__device__ int coop_wait(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_flag, uint32_t sec) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   if (tid == 0) {
     coop_publish(P, s_q);
@@ -516,7 +513,7 @@ __device__ __forceinline__ int coop_wait(const PlanArgs& P, const Arrays& S, uin
 }
 
 // COOP_RETRY: every dirty agent whose pair still reads pending is queued again on the needed queue
-__device__ __forceinline__ void coop_requeue(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
+__device__ void coop_requeue(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (S.NHC[k] <= NH_STAY) continue;
@@ -536,7 +533,7 @@ __device__ __forceinline__ void coop_requeue(const PlanArgs& P, const Arrays& S,
 // Next hops are missing (refresh_codes returned nonzero and queued them). Coop mode: wait for the
 // workers and re-run the refresh until nothing is missing (true: continue in the kernel). Otherwise,
 // or if the workers do not answer, false: the caller exits for a host-side K3 pass.
-__device__ __forceinline__ bool coop_resolve(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need, uint32_t* s_flag,
+__device__ bool coop_resolve(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t* s_need, uint32_t* s_flag,
                              uint32_t sec) {
   if (!P.coop) return false;
   for (int it = 0; it < 1024; ++it) {
@@ -556,7 +553,7 @@ __device__ __forceinline__ bool coop_resolve(const PlanArgs& P, const Arrays& S,
 // speculatively (no exit): the planner exits only when a firing actually needs a code, and
 // that one K3 launch then resolves everything queued so far. Half the queue stays free for the
 // pairs an exit needs.
-__device__ __forceinline__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
+__device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (spec_full(P, s_q)) break;
@@ -582,10 +579,10 @@ __device__ __forceinline__ void rules_prefetch(const PlanArgs& P, const Arrays& 
 // rules_prefetch restricted to the agents a firing changed (rule 3: b and s, rule 4: the cycle):
 // only their goals, hence their next hops and successors, moved, so only their pairs are new.
 // After rules_init (SUCC valid).
-__device__ __forceinline__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab,
+__device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab,
                                   uint32_t hops, uint32_t h0 = 0u, uint32_t* end = nullptr,
                                   uint32_t* endh = nullptr);
-__device__ __forceinline__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab);
+__device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab);
 
 // coop mode: agent k will be idle at `cell` (its delivery): a worker predicts its next task and walks that
 // task's pickup -> delivery chain ahead of the assignment (s_q[8]: entries queued, PlanArgs::QP)
@@ -626,7 +623,7 @@ __device__ __forceinline__ void prefetch_changed(const PlanArgs& P, const Arrays
   if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) prefetch_pair(P, vs, S.G[k], tab, s_q);
 }
 
-__device__ __forceinline__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t* s_q, const uint32_t* lst,
+__device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t* s_q, const uint32_t* lst,
                                     uint32_t cnt) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t i = tid; i < cnt; i += bd) prefetch_changed(P, S, s_q, lst[i]);
@@ -638,7 +635,7 @@ __device__ __forceinline__ void rules_prefetch_list(const PlanArgs& P, const Arr
 // the DAG ahead of u is where the agent goes next. Its cells are queued level by level (frontier
 // capped at DAG_WIDTH; a resolved cell contributes only the cell its code points at), so a path
 // resolves several cells per A* latency instead of one.
-__device__ __forceinline__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab) {
+__device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab) {
   constexpr uint32_t DAG_WIDTH = 16;  // array bound; P.dag_width caps the frontier (default 4)
   const uint32_t dwid = P.dag_width ? min(P.dag_width, DAG_WIDTH) : 4u;
   const uint16_t* dt = P.dist + (uint64_t)tab * P.nstride;
@@ -680,7 +677,7 @@ __device__ __forceinline__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, u
 // Walk the resolved codes toward g from cell u, which lies h0 resolved hops past the agent's next cell,
 // until hop `hops`; queue the first unresolved pair (and the DAG past it). Returns the hops left when the
 // walk reached g, else 0. *end / *endh (if given): the cell the walk stopped at and its hop index.
-__device__ __forceinline__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab,
+__device__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab,
                                   uint32_t hops, uint32_t h0, uint32_t* end, uint32_t* endh) {
   uint32_t h = h0;
   uint32_t left = 0;
@@ -716,7 +713,7 @@ __device__ __forceinline__ uint32_t walk_prefetch(const PlanArgs& P, uint32_t* s
 //    (prefetch_ext bit 0);
 //  * an agent heading to a pickup whose walk reaches it continues along the delivery leg: the
 //    state machine switches its goal there (tswap.rs:113-118) (prefetch_ext bit 1).
-__device__ __forceinline__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t hops) {
+__device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint32_t hops) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (spec_full(P, s_q)) break;
@@ -780,81 +777,52 @@ __device__ __forceinline__ void nextnext_prefetch(const PlanArgs& P, const Array
 }
 
 // Serial movement phase (tswap.rs:257-285) — used when cells are shared by several agents
-// (duplicate start cells). Scans agents from i0; returns the agent it stopped at (n when done) and sets
-// *miss to 1 on an unresolved next hop, 2 on a goal without a table. Kept out of line, with its inputs
-// by value (no reference to PlanArgs / Arrays / the LDS control block escapes, so the kernel keeps
-// PlanArgs in its kernel-argument registers): with this cold path inlined, the diagnostic build's planner
-// hung in the first rules phase of every plan (round 6, scripts/inline_bisect.sh).
-__device__ __attribute__((noinline)) uint32_t walk_move(uint32_t n, uint32_t W, const uint8_t* nh, uint64_t nstride,
-                                                        uint32_t coop, uint32_t* V, const uint32_t* G, uint8_t* NHC,
-                                                        const int32_t* GT, uint32_t* OCC, uint32_t i0, uint32_t* miss) {
-  auto code_of = [&](uint32_t k) -> int {  // lookup_code
-    const uint8_t c = NHC[k];
-    if (c <= NH_STAY) return c;
-    const int32_t tab = GT[k];
-    if (tab < 0) return -2;
-    const uint8_t* p = nh + (uint64_t)tab * nstride + V[k];
-    uint8_t code = *p;
-    if (coop && (code == NH_PENDING || code == NH_PENDING_S)) {  // nh_code's agent-scope re-read
-      const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      code = (uint8_t)(w >> (8u * (uint32_t)((uintptr_t)p & 3u)));
-    }
-    if (code <= NH_STAY) {
-      NHC[k] = code;
-      return code;
-    }
-    return -1;
-  };
-  auto rescan = [&](uint32_t cell) {  // occ_rescan
-    uint32_t lowest = OCC_NONE, cnt = 0;
-    for (uint32_t k = 0; k < n; ++k)
-      if (V[k] == cell) {
-        if (cnt == 0) lowest = k;
-        ++cnt;
-      }
-    OCC[cell] = cnt == 0 ? OCC_NONE : (lowest | (cnt > 1 ? OCC_FLAG : 0u));
-  };
-  uint32_t i = i0;
+// (duplicate start cells); false on an unresolved next hop.
+__device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
+  const uint32_t n = P.n, W = P.W;
+  uint32_t i = ctl.i;
   for (; i < n; ++i) {
-    const uint32_t vi = V[i], gi = G[i];
+    const uint32_t vi = S.V[i], gi = S.G[i];
     if (vi == gi) continue;
-    const int code = code_of(i);
+    const int code = lookup_code(P, S, i);
     if (code < 0) {
-      *miss = code == -2 ? 2u : 1u;
-      return i;
+      ctl.miss = code == -2 ? 2u : 1u;
+      ctl.i = i;
+      return false;
     }
     const uint32_t u = step_cell(vi, (uint32_t)code, W);
-    const uint32_t o = OCC[u];
+    const uint32_t o = S.OCC[u];
     if (o == OCC_NONE) {  // rule 2: move
-      V[i] = u;
-      NHC[i] = NHC_DIRTY;
-      OCC[u] = i;
-      if (OCC[vi] & OCC_FLAG) rescan(vi);
-      else OCC[vi] = OCC_NONE;
+      S.V[i] = u;
+      S.NHC[i] = NHC_DIRTY;
+      S.OCC[u] = i;
+      if (S.OCC[vi] & OCC_FLAG) occ_rescan(P, S, vi);
+      else S.OCC[vi] = OCC_NONE;
     } else if ((o & OCC_IDX) != i) {
       const uint32_t j = o & OCC_IDX;
-      const uint32_t vj = V[j], gj = G[j];
+      const uint32_t vj = S.V[j], gj = S.G[j];
       if (vj != gj) {
-        const int cj = code_of(j);
+        const int cj = lookup_code(P, S, j);
         if (cj < 0) {
-          *miss = cj == -2 ? 2u : 1u;
-          return i;
+          ctl.miss = cj == -2 ? 2u : 1u;
+          ctl.i = i;
+          return false;
         }
         if (step_cell(vj, (uint32_t)cj, W) == vi) {  // mutual swap (:273-278)
-          V[i] = vj;
-          V[j] = vi;
-          NHC[i] = NHC_DIRTY;
-          NHC[j] = NHC_DIRTY;
-          if (OCC[vi] & OCC_FLAG) rescan(vi);
-          else OCC[vi] = j;
-          if (o & OCC_FLAG) rescan(vj);
-          else OCC[vj] = i;
+          S.V[i] = vj;
+          S.V[j] = vi;
+          S.NHC[i] = NHC_DIRTY;
+          S.NHC[j] = NHC_DIRTY;
+          if (S.OCC[vi] & OCC_FLAG) occ_rescan(P, S, vi);
+          else S.OCC[vi] = j;
+          if (o & OCC_FLAG) occ_rescan(P, S, vj);
+          else S.OCC[vj] = i;
         }
       }
     }
   }
-  return n;
+  ctl.i = n;
+  return true;
 }
 
 }  // namespace
@@ -2195,16 +2163,12 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
       __syncthreads();
     } else if (sec == SEC_MOVE && P.has_dups) {
       if (tid == 0) {
-        uint32_t miss = 0;
-        const uint32_t at = walk_move(n, W, P.nh, P.nstride, P.coop, S.V, S.G, S.NHC, S.GT, S.OCC, s_ctl.i, &miss);
-        s_ctl.miss = miss;
-        if (miss == 0u) {
+        s_ctl.miss = 0;
+        if (walk_move(P, S, s_ctl)) {
           s_ctl.section = SEC_RECORD;
           s_ctl.i = 0;
-        } else {
-          s_ctl.i = at;
         }
-        if (miss == 2u) atomicOr(&P.ctl->err, ERR_NO_TABLE);
+        if (s_ctl.miss == 2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
       }
       __syncthreads();
       if (s_ctl.miss) {
