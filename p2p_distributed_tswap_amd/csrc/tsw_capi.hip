@@ -270,6 +270,7 @@ struct tsw_ctx {
   DevStatus* d_stat = nullptr;
   DevStatus* h_stat = nullptr;   // pinned, D2H
   PlanCtl* d_ctl = nullptr;
+  PlanArgs* d_pargs = nullptr;  // k_plan reads its arguments from here
   PlanCtl* h_ctl = nullptr;      // pinned
   unsigned long long* d_ticks = nullptr;
   uint32_t* d_dtag = nullptr;  // TSW_PLAN_DEBUG: per-agent change tags (PlanArgs::dtag)
@@ -1510,7 +1511,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     }
     {
       Timer t(c, CAT_WALK);
-      HIPCHK(launch_plan(P, coop ? &W : nullptr, wblocks, lds, block, c->s));
+      HIPCHK(launch_plan(P, c->d_pargs, coop ? &W : nullptr, wblocks, lds, block, c->s));
       c->st.plan_block = block;
     }
     c->st.walker_launches++;
@@ -2019,6 +2020,7 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
   if ((e = hipHostMalloc(&c->h_stat, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned status", e);
   if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
+  if ((e = hipMalloc(&c->d_pargs, sizeof(PlanArgs))) != hipSuccess) return fail("malloc plan args", e);
   if ((e = hipMalloc(&c->d_ticks, 40 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
   if ((e = hipMemsetAsync(c->d_ticks, 0, 40 * sizeof(unsigned long long), c->s)) != hipSuccess)
     return fail("memset ticks", e);
@@ -2051,7 +2053,7 @@ void tsw_destroy(tsw_ctx* c) {
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
   fre(c->d_gt); fre(c->d_dec); fre(c->d_mu); fre(c->d_dups); fre(c->d_onc); fre(c->d_candc); fre(c->d_f1); fre(c->d_f2);
   if (c->h_dups) (void)hipHostFree(c->h_dups);
-  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_ticks); fre(c->d_dtag); fre(c->d_live); fre(c->d_klt); fre(c->d_kpos); fre(c->d_kbox); fre(c->d_kcnt); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
+  fre(c->d_task); fre(c->d_occ); fre(c->d_nhc); fre(c->d_ctl); fre(c->d_pargs); fre(c->d_ticks); fre(c->d_dtag); fre(c->d_live); fre(c->d_klt); fre(c->d_kpos); fre(c->d_kbox); fre(c->d_kcnt); fre(c->d_pick); fre(c->d_dlv); fre(c->d_unused);
   fre(c->d_rec); fre(c->d_grec); fre(c->d_tmp_a); fre(c->d_tmp_b);
   fre(c->d_cc); fre(c->d_QS); fre(c->d_QT); fre(c->d_QH); fre(c->d_QP); fre(c->d_pred); fre(c->d_wf); fre(c->d_govf); fre(c->d_mg_grp); fre(c->d_mg_wl); fre(c->d_mg_anch);
   if (c->h_cc) (void)hipHostFree(c->h_cc);

@@ -19,10 +19,12 @@ enum : uint32_t {
 };
 enum : uint32_t { PLAN_RUNNING = 0, PLAN_NEED_QUERIES = 1, PLAN_DONE = 2, PLAN_ERROR = 3 };
 enum : uint32_t { MODE_MAPD = 0, MODE_STEP = 1 };
-// k_plan's workgroup size cap (its __launch_bounds__). At 512 threads (2 waves per SIMD) a wave may use
-// 256 VGPRs: the planner's live state fits with no spill and no scratch; at 1,024 it was capped at 128
-// VGPRs with 67 spilled and 944 B of scratch per lane (round 6; scripts/isa_scratch.py).
-constexpr uint32_t PLAN_BLOCK_MAX = 512;
+// k_plan's workgroup size cap (its __launch_bounds__). The planner's live state peaks at ~195 VGPRs; at
+// 1,024 threads (4 waves per SIMD) a wave gets 128, so ~60 VGPRs spill, but its latency-bound per-agent
+// passes (K4 scan, walk-ahead, movement rounds) run one agent per thread on C3. Round 6 measured the
+// spill-free 512-thread bound 3-6 % slower end to end (ASSIGN +25 ms, PRE1 +40 ms per busy C3 plan:
+// two agents per thread, one after the other), profiles/r6/ab_r6_pg.txt.
+constexpr uint32_t PLAN_BLOCK_MAX = 1024;
 constexpr uint32_t TASK_TAKEN = 0xFFFFFFFFu;  // PlanArgs::live entry of an assigned task
 
 // Persisted in device memory between launches (exact resume point).
@@ -200,7 +202,7 @@ WorkerCfg worker_config(const DevGrid& G, int num_cu, uint32_t n_agents, uint32_
 
 // The plan dispatch: workgroup 0 runs k_plan's planner (block threads, lds bytes of dynamic LDS);
 // with W (coop mode) workgroups 1..worker_blocks run W->wpb K3 worker waves each.
-hipError_t launch_plan(const PlanArgs& P, const WorkerArgs* W, uint32_t worker_blocks, size_t lds, uint32_t block,
-                       hipStream_t s);
+hipError_t launch_plan(const PlanArgs& P, PlanArgs* d_args, const WorkerArgs* W, uint32_t worker_blocks, size_t lds,
+                       uint32_t block, hipStream_t s);
 
 }  // namespace tsw

@@ -4,19 +4,19 @@
 
 namespace tsw {
 
-hipError_t launch_plan_v0(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_v0(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                           hipStream_t s);
-hipError_t launch_plan_v1(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_v1(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                           hipStream_t s);
-hipError_t launch_plan_v2(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_v2(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                           hipStream_t s);
-hipError_t launch_plan_v3(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_v3(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                           hipStream_t s);
-hipError_t launch_plan_v4(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_v4(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                           hipStream_t s);
-hipError_t launch_plan_v5(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_v5(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                           hipStream_t s);
-hipError_t launch_plan_v6(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_v6(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                           hipStream_t s);
 
 // occupancy in the k_plan encoding: lowest agent index | OCC_FLAG if shared, OCC_NONE if empty
@@ -74,20 +74,22 @@ hipError_t launch_occ(const uint32_t* v, uint32_t n, uint32_t* occ, uint32_t* cn
   return hipGetLastError();
 }
 
-hipError_t launch_plan(const PlanArgs& P, const WorkerArgs* W, uint32_t worker_blocks, size_t lds, uint32_t block,
-                       hipStream_t s) {
+hipError_t launch_plan(const PlanArgs& P, PlanArgs* d_args, const WorkerArgs* W, uint32_t worker_blocks, size_t lds,
+                       uint32_t block, hipStream_t s) {
   WorkerArgs none{};
   const WorkerArgs& A = (W && P.coop) ? *W : none;
   const uint32_t grid = 1u + ((W && P.coop) ? worker_blocks : 0u);
   if (grid > 1u && ((size_t)A.wpb * A.lds_per_wave > lds || A.wpb * 64u > block)) return hipErrorInvalidValue;
   const bool mu = P.occ_lds && P.mu_lds;
-  if (P.agents_lds && mu) return launch_plan_v0(P, A, grid, lds, block, s);
-  if (P.agents_lds && P.occ_lds) return launch_plan_v1(P, A, grid, lds, block, s);
-  if (P.agents_lds) return launch_plan_v2(P, A, grid, lds, block, s);
-  if (P.part_lds == PART_PG && !P.occ_lds) return launch_plan_v3(P, A, grid, lds, block, s);
-  if (mu) return launch_plan_v4(P, A, grid, lds, block, s);
-  if (P.occ_lds) return launch_plan_v5(P, A, grid, lds, block, s);
-  return launch_plan_v6(P, A, grid, lds, block, s);
+  // the kernel reads its arguments from d_args (stream order: after the previous dispatch has finished)
+  if (hipError_t e = hipMemcpyAsync(d_args, &P, sizeof(PlanArgs), hipMemcpyHostToDevice, s); e != hipSuccess) return e;
+  if (P.agents_lds && mu) return launch_plan_v0(d_args, A, grid, lds, block, s);
+  if (P.agents_lds && P.occ_lds) return launch_plan_v1(d_args, A, grid, lds, block, s);
+  if (P.agents_lds) return launch_plan_v2(d_args, A, grid, lds, block, s);
+  if (P.part_lds == PART_PG && !P.occ_lds) return launch_plan_v3(d_args, A, grid, lds, block, s);
+  if (mu) return launch_plan_v4(d_args, A, grid, lds, block, s);
+  if (P.occ_lds) return launch_plan_v5(d_args, A, grid, lds, block, s);
+  return launch_plan_v6(d_args, A, grid, lds, block, s);
 }
 
 }  // namespace tsw

@@ -848,7 +848,12 @@ __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
 // LDS — carved unconditionally, so its accesses compile to ds_* instead of flat instructions (a flat
 // access waits for every outstanding global load as well). Otherwise part_lds picks arrays at run time.
 template <bool AG, bool OC, bool MUL, bool PG>
-__global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs Wk) {
+// PlanArgs lives in device memory (written by launch_plan before the dispatch) and is read through a
+// const restrict pointer: the kernel body's field loads are scalar loads, and the out-of-line helpers get
+// a reference to it instead of to a private copy (a by-value kernel argument whose address reaches a
+// non-inlined call is copied to scratch, and every field access then became a scratch load; round 6).
+__global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restrict__ Pg, WorkerArgs Wk) {
+  const PlanArgs& P = *Pg;
   extern __shared__ __align__(16) uint8_t smem[];
   if (blockIdx.x != 0) {  // coop mode: a K3 worker workgroup (tsw_worker.h), Wk.wpb single-wave workers
     const uint32_t w = threadIdx.x >> 6;
@@ -2490,7 +2495,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(PlanArgs P, WorkerArgs 
 
 
 template <bool AG, bool OC, bool MUL, bool PG = false>
-hipError_t launch_plan_t(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_t(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                                 hipStream_t s) {
   hipError_t e = hipFuncSetAttribute((const void*)k_plan<AG, OC, MUL, PG>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

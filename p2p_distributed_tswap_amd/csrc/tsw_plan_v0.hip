@@ -2,7 +2,7 @@
 #include "tsw_plan_kernel.h"
 
 namespace tsw {
-hipError_t launch_plan_v0(const PlanArgs& P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
+hipError_t launch_plan_v0(const PlanArgs* P, const WorkerArgs& W, uint32_t grid, size_t lds, uint32_t block,
                           hipStream_t s) {
   return launch_plan_t<true, true, true, false>(P, W, grid, lds, block, s);
 }
