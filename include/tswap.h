@@ -34,7 +34,7 @@
  *     entries, past that TSW_EOVERFLOW
  *   - tsw_decide: at most 1024 entries in one agent's nearby list (TSW_EOVERFLOW;
  *     get_nearby, decentralized/agent.rs:108-153, has no bound)
- *   - goal tables: table_budget_bytes (3 B per cell per goal). Tables not used by
+ *   - goal tables: table_budget_bytes (2 B per cell per goal). Tables not used by
  *     the current call are evicted least-recently-used first; TSW_ENOMEM only
  *     when the goals of ONE call do not fit.
  *
@@ -100,7 +100,7 @@ typedef struct {
 typedef struct {
     int32_t device;              /* HIP device ordinal (default 0)                                  */
     uint32_t flags;              /* TSW_F_* below                                                   */
-    uint64_t table_budget_bytes; /* cap for distance+next-hop tables, 3 B per cell per goal
+    uint64_t table_budget_bytes; /* cap for detour-byte+next-hop tables, 2 B per cell per goal
                                     (0 = half of the device's free memory at tsw_create)            */
     uint32_t watchdog_ms;        /* plan calls: if the planner records no timestep for this long,
                                     the call finishes in exit mode (0 = 10000)                      */

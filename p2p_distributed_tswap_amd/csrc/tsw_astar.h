@@ -513,36 +513,31 @@ __device__ __forceinline__ void rpush(uint64_t& R, uint32_t& len, uint64_t e, co
   ++len;
 }
 
-// Detour bytes of a goal's K1 table for astar_wave_par<*, *, 1>: DT[c] = (D[c] - |c - goal|_1) / 2
-// (D and the Manhattan distance share parity on a 4-grid), 255 when that is >= 255 or c is blocked /
-// unreachable. One wave; D is the slot's u16 table. Only the cells of the box [x0, x1] x [y0, y1] are
-// written: the caller passes the bounding box of the query's ellipse {x : |x - v| + |x - goal| <= d*},
+// Detour bytes of a goal for astar_wave_par<*, *, 1>: DT[c] = (D[c] - |c - goal|_1) / 2 (D and the Manhattan
+// distance share parity on a 4-grid), 255 when that is >= 255 or c is blocked / unreachable — the table
+// store's format (round 6), copied from the goal's store slot DTg. Only the cells of the box [x0, x1] x
+// [y0, y1] are copied: the caller passes the bounding box of the query's ellipse {x : |x - v| + |x - goal| <= d*},
 // outside which every cell has f = g + h > d* and so can never pass the DAG test (g + D = d*) whatever
-// DT holds there. Lanes walk the box's cells in row-major order, STAGE_INFLIGHT loads in flight per
-// lane (the staging is a chain of global round trips in front of the query's first pop: C3 spent
-// ~38 us per staging with 4 in flight).
+// DT holds there. Lanes walk the box's cells in row-major order, STAGE_INFLIGHT loads in flight per lane
+// (the staging is a chain of global round trips in front of the query's first pop).
 constexpr uint32_t STAGE_INFLIGHT = 8u;
-__device__ __forceinline__ void stage_detour(uint8_t* DT, const uint16_t* D, uint32_t W, uint32_t goal, uint32_t x0,
-                                             uint32_t x1, uint32_t y0, uint32_t y1, uint32_t lane) {
-  const uint32_t gy = goal / W, gx = goal - gy * W;
+__device__ __forceinline__ void stage_detour(uint8_t* DT, const uint8_t* DTg, uint32_t W, uint32_t x0, uint32_t x1,
+                                             uint32_t y0, uint32_t y1, uint32_t lane) {
   const uint32_t bw = x1 - x0 + 1u, nb = bw * (y1 - y0 + 1u);
   const float inv = 1.0f / (float)bw;
   for (uint32_t i0 = lane; i0 < nb; i0 += 64u * STAGE_INFLIGHT) {
-    uint32_t cell[STAGE_INFLIGHT], d[STAGE_INFLIGHT], x[STAGE_INFLIGHT], y[STAGE_INFLIGHT];
+    uint32_t cell[STAGE_INFLIGHT], d[STAGE_INFLIGHT];
 #pragma unroll
     for (uint32_t u = 0; u < STAGE_INFLIGHT; ++u) {
       const uint32_t i = i0 + 64u * u;
       const uint32_t r = fast_div(i < nb ? i : 0u, bw, inv);
-      y[u] = y0 + r;
-      x[u] = x0 + ((i < nb ? i : 0u) - r * bw);
-      cell[u] = y[u] * W + x[u];
-      d[u] = D[cell[u]];
+      cell[u] = (y0 + r) * W + x0 + ((i < nb ? i : 0u) - r * bw);
+      d[u] = DTg[cell[u]];
     }
 #pragma unroll
     for (uint32_t u = 0; u < STAGE_INFLIGHT; ++u) {
       if (i0 + 64u * u >= nb) break;
-      const uint32_t man = (x[u] > gx ? x[u] - gx : gx - x[u]) + (y[u] > gy ? y[u] - gy : gy - y[u]);
-      DT[cell[u]] = (uint8_t)(d[u] == 0xFFFFu || d[u] < man ? 255u : min((d[u] - man) >> 1, 255u));
+      DT[cell[u]] = (uint8_t)d[u];
     }
   }
 }
@@ -552,7 +547,7 @@ __device__ __forceinline__ void stage_detour(uint8_t* DT, const uint16_t* D, uin
 // PROF: pr[0..4] = pops, clocks in pops, in relaxations, in pushes, pushes (TSW_ASTAR_PROF)
 //
 // DAG early exit (DAG = 1: the goal's detour bytes DT staged in LDS, see stage_detour; DAG = 2: the
-// goal's u16 K1 table DG read beside the g-score words; 0: off). Exact, from these facts about this
+// same bytes read from the goal's table-store slot DG beside the g-score words; 0: off). Exact, from these facts about this
 // A* (consistent Manhattan heuristic, no closed set, keys (f, then smaller g)):
 //  * a node n is relaxed at most once with its optimal g = d_s(n) (later relaxations need a strictly
 //    smaller g), and that relaxation fixes came_from(n) — hence its label — for good;
@@ -571,7 +566,7 @@ template <int GSM, bool PROF, int DAG = 0, bool REG = true>
 __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, uint32_t goal, uint32_t tag,
                                                   uint64_t* Hp, uint32_t hcap, uint32_t* GS, uint8_t* GB,
                                                   const uint32_t* FB, int32_t* len_out, unsigned long long* pr,
-                                                  const uint8_t* DT = nullptr, const uint16_t* DG = nullptr,
+                                                  const uint8_t* DT = nullptr, const uint8_t* DG = nullptr,
                                                   uint32_t* npop = nullptr, uint32_t dag_mask = 15u,
                                                   uint32_t reg_max = REG_HEAP_MAX) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -605,17 +600,16 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
     *len_out = -2;
     return NH_UNKNOWN;
   }
-  // DAG early exit: d* and whether it applies (the start reaches the goal; with detour bytes every DAG
-  // node's detour (D - h) / 2 <= d* / 2 must fit below the saturated 255)
+  // DAG early exit: d* = h0 + 2 * detour(v), applicable when the start reaches the goal with an exact
+  // detour byte. A DAG node n lies on a shortest start -> goal path, and along such a path the detour
+  // (D - h) / 2 never grows (D drops by 1 per hop, h changes by 1), so detour(n) <= detour(v) < 255: the
+  // test below skips saturated bytes (255) without skipping any DAG node.
   uint32_t dstar = 0xFFFFFFFFu;
   bool ee = false;
-  if constexpr (DAG == 1) {
-    const uint32_t dv = DT[v];
+  if constexpr (DAG != 0) {
+    const uint32_t dv = DAG == 1 ? DT[v] : DG[v];
     dstar = h0 + 2u * dv;
-    ee = dv != 255u && dstar <= 508u;
-  } else if constexpr (DAG == 2) {
-    dstar = DG[v];
-    ee = dstar != 0xFFFFu;
+    ee = dv != 255u;
   }
   // the heap starts in registers (see rpop): the start entry at the root (lane 63); reg_max = 0 keeps
   // it in the LDS array throughout (A/B). REG = false compiles the register heap out: on grids whose
@@ -741,13 +735,10 @@ __device__ __forceinline__ uint8_t astar_wave_par(const DevGrid& G, uint32_t v, 
           const uint64_t en = reg ? R : Hp[j < len ? j : 0u];
           const uint32_t lo = (uint32_t)en, ex = lo >> 16, ey = lo & 0x7FFu, eg = hk(en) & 0x7FFFu;
           const uint32_t ec = ey * W + ex;
-          bool d;
-          if constexpr (DAG == 1) {  // D = Manhattan to the goal + 2 * detour
-            const uint32_t eh = (ex > gx ? ex - gx : gx - ex) + (ey > gy ? ey - gy : gy - ey);
-            d = eg + eh + 2u * (uint32_t)DT[ec] == dstar;
-          } else {
-            d = eg + (uint32_t)DG[ec] == dstar;
-          }
+          // D = Manhattan to the goal + 2 * detour (DAG 1: LDS-staged bytes, DAG 2: the store slot's)
+          const uint32_t eh = (ex > gx ? ex - gx : gx - ex) + (ey > gy ? ey - gy : gy - ey);
+          const uint32_t db = DAG == 1 ? (uint32_t)DT[ec] : (uint32_t)DG[ec];
+          bool d = db != 255u && eg + eh + 2u * db == dstar;
           d = d && j < len;
           const uint32_t el = (lo >> 12) & 3u;
           const uint64_t gm = ballot64(d && ec == goal);

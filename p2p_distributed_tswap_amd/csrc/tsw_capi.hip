@@ -206,8 +206,10 @@ struct tsw_ctx {
   // iff h_tab_goal[slot] != NO_GOAL. Slots of evicted tables sit on tab_free for reuse.
   uint64_t tstride = 0;
   uint32_t tab_cap = 0, tab_count = 0, tab_live = 0;
-  uint16_t* d_dist = nullptr;
-  uint8_t* d_nh = nullptr;
+  uint8_t* d_dt = nullptr;       // detour bytes per (slot, cell) (tsw_internal.h), 1 B / cell / goal
+  uint8_t* d_nh = nullptr;       // next-hop codes per (slot, cell), 1 B / cell / goal
+  uint16_t* d_ktmp = nullptr;    // K1 output of one build batch (u16 tables, tstride each), classified into the store
+  size_t ktmp_tabs = 0;
   int32_t* d_goal_tab = nullptr;
   std::vector<int32_t> h_goal_tab;
   std::vector<uint32_t> h_tab_goal;
@@ -308,7 +310,7 @@ struct tsw_ctx {
   uint32_t* d_grec = nullptr;
   size_t grec_cap = 0;
   // temporaries
-  uint32_t *d_tmp_a = nullptr, *d_tmp_b = nullptr;
+  uint32_t *d_tmp_a = nullptr, *d_tmp_b = nullptr, *d_tmp_c = nullptr;
   size_t tmp_cap = 0;
 
   // stats / timing
@@ -446,9 +448,29 @@ int ensure_tmp(tsw_ctx* c, size_t k) {
   if (k <= c->tmp_cap && c->d_tmp_a) return TSW_OK;
   size_t ca = c->tmp_cap, cb = c->tmp_cap;
   HIPCHK(hipStreamSynchronize(c->s));
+  size_t cc = c->tmp_cap;
   HIPCHK(dgrow(c->d_tmp_a, ca, k));
   HIPCHK(dgrow(c->d_tmp_b, cb, k));
-  c->tmp_cap = std::min(ca, cb);
+  HIPCHK(dgrow(c->d_tmp_c, cc, k));
+  c->tmp_cap = std::min(ca, std::min(cb, cc));
+  return TSW_OK;
+}
+
+// K1 output buffer of a table-build batch: u16 tables of KTMP_BYTES at most (C5's 2 MiB tables: 1,024
+// goals per batch), at least one table. Returns the batch size in tables.
+constexpr size_t KTMP_BYTES = (size_t)2 << 30;
+int ensure_ktmp(tsw_ctx* c, size_t want, size_t* batch) {
+  const size_t per = (size_t)c->tstride * 2u;
+  const size_t b = std::max<size_t>(1, std::min(want, KTMP_BYTES / per));
+  if (c->ktmp_tabs < b || !c->d_ktmp) {
+    HIPCHK(hipStreamSynchronize(c->s));
+    if (c->d_ktmp) HIPCHK(hipFree(c->d_ktmp));
+    c->d_ktmp = nullptr;
+    c->ktmp_tabs = 0;
+    HIPCHK(hipMalloc(&c->d_ktmp, b * per));
+    c->ktmp_tabs = b;
+  }
+  *batch = b;
   return TSW_OK;
 }
 
@@ -993,25 +1015,25 @@ constexpr uint32_t NO_GOAL = 0xFFFFFFFFu;
 // Grow the device store to at least `need` slots (never past the budget; callers check).
 int grow_store(tsw_ctx* c, size_t need) {
   if (need <= c->tab_cap) return TSW_OK;
-  const uint64_t max_tabs = c->table_budget / (c->tstride * 3ull);
+  const uint64_t max_tabs = c->table_budget / (c->tstride * 2ull);
   size_t nc = std::max<size_t>(need, std::max<size_t>((size_t)c->tab_cap * 2, 64));
   nc = std::max<size_t>(need, std::min<size_t>(nc, (size_t)max_tabs));
   HIPCHK(hipStreamSynchronize(c->s));
-  uint16_t* nd = nullptr;
+  uint8_t* nd = nullptr;
   uint8_t* nn = nullptr;
-  HIPCHK(hipMalloc(&nd, nc * c->tstride * 2ull));
+  HIPCHK(hipMalloc(&nd, nc * c->tstride));
   if (hipError_t e = hipMalloc(&nn, nc * c->tstride); e != hipSuccess) {
     (void)hipFree(nd);
     RET(TSW_ENOMEM, std::string("table store growth: ") + hipGetErrorString(e));
   }
   if (c->tab_count) {
-    HIPCHK(hipMemcpyAsync(nd, c->d_dist, (size_t)c->tab_count * c->tstride * 2ull, hipMemcpyDeviceToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(nd, c->d_dt, (size_t)c->tab_count * c->tstride, hipMemcpyDeviceToDevice, c->s));
     HIPCHK(hipMemcpyAsync(nn, c->d_nh, (size_t)c->tab_count * c->tstride, hipMemcpyDeviceToDevice, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
   }
-  if (c->d_dist) HIPCHK(hipFree(c->d_dist));
+  if (c->d_dt) HIPCHK(hipFree(c->d_dt));
   if (c->d_nh) HIPCHK(hipFree(c->d_nh));
-  c->d_dist = nd;
+  c->d_dt = nd;
   c->d_nh = nn;
   c->tab_cap = (uint32_t)nc;
   c->h_tab_goal.resize(nc, NO_GOAL);
@@ -1044,7 +1066,7 @@ void stamp_and_collect(tsw_ctx* c, const uint32_t* goals, size_t k, std::vector<
 // Evicted goals lose their table (goal_tab -1); later calls rebuild them on demand.
 int reserve_slots(tsw_ctx* c, size_t k, std::vector<uint32_t>& slots) {
   slots.clear();
-  const uint64_t max_tabs = c->table_budget / (c->tstride * 3ull);
+  const uint64_t max_tabs = c->table_budget / (c->tstride * 2ull);
   while (slots.size() < k && !c->tab_free.empty()) {
     slots.push_back(c->tab_free.back());
     c->tab_free.pop_back();
@@ -1113,12 +1135,9 @@ int build_new_tables(tsw_ctx* c, const std::vector<uint32_t>& newg, const std::v
                      bool tableless_ok) {
   std::vector<uint32_t>& lg = c->h_lpt_goals;
   std::vector<uint32_t>& ls = c->h_lpt_slots;
-  lg = newg;
-  ls = slots;
-  bfs_lpt_order(c, lg, ls);
+  lg.resize(newg.size());
+  ls.resize(newg.size());
   TRY(ensure_tmp(c, newg.size()));
-  HIPCHK(hipMemcpyAsync(c->d_tmp_a, lg.data(), lg.size() * 4, hipMemcpyHostToDevice, c->s));
-  HIPCHK(hipMemcpyAsync(c->d_tmp_b, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, c->s));
   if (tableless_ok) {
     if (newg.size() > c->govf_cap || !c->d_govf) {
       HIPCHK(hipStreamSynchronize(c->s));
@@ -1126,8 +1145,25 @@ int build_new_tables(tsw_ctx* c, const std::vector<uint32_t>& newg, const std::v
     }
     HIPCHK(hipMemsetAsync(c->d_govf, 0, newg.size(), c->s));
   }
-  TRY(run_bfs(c, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh,
-              tableless_ok ? c->d_govf : nullptr));
+  // K1 in batches into the u16 buffer, each batch classified into the store (codes + detour bytes):
+  // the u16 tables never live in the store (round 6: 3 -> 2 B per cell per goal; C5 79.5 -> ~57 GiB)
+  // (launch order per batch: longest BFS first, bfs_lpt_order; lg / ls hold the ordered goals / store slots)
+  size_t batch = 0;
+  TRY(ensure_ktmp(c, newg.size(), &batch));
+  for (size_t i0 = 0; i0 < newg.size(); i0 += batch) {
+    const uint32_t nb = (uint32_t)std::min(batch, newg.size() - i0);
+    std::vector<uint32_t> bg(newg.begin() + i0, newg.begin() + i0 + nb), bs(slots.begin() + i0, slots.begin() + i0 + nb);
+    bfs_lpt_order(c, bg, bs);
+    std::copy(bg.begin(), bg.end(), lg.begin() + i0);
+    std::copy(bs.begin(), bs.end(), ls.begin() + i0);
+    HIPCHK(hipMemcpyAsync(c->d_tmp_a + i0, lg.data() + i0, (size_t)nb * 4, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_tmp_b + i0, ls.data() + i0, (size_t)nb * 4, hipMemcpyHostToDevice, c->s));
+    TRY(run_bfs(c, c->d_tmp_a + i0, nullptr, nb, c->d_ktmp, c->tstride, nullptr,
+                tableless_ok ? c->d_govf + i0 : nullptr));
+    HIPCHK(launch_classify_dt(c->G, c->d_tmp_a + i0, nullptr, c->d_tmp_b + i0, nb, c->d_ktmp, c->tstride, c->d_nh,
+                              c->d_dt, c->tstride, c->s));
+    HIPCHK(hipStreamSynchronize(c->s));  // the host copies bg / bs and the mg group offsets are reused next batch
+  }
   c->st.bfs_goals += newg.size();
   c->st.bfs_launches++;
   for (uint32_t s : slots) c->h_tab_tableless[s] = 0;
@@ -1141,12 +1177,35 @@ int build_new_tables(tsw_ctx* c, const std::vector<uint32_t>& newg, const std::v
       const uint32_t slot = ls[i];
       c->h_tab_tableless[slot] = 1;
       ++c->st.tableless_goals;
-      // no distance (DAG prefetch reads INF: nothing to follow) and every code unresolved (K3)
-      HIPCHK(hipMemsetAsync(c->d_dist + (size_t)slot * c->tstride, 0xFF, c->tstride * 2, c->s));
+      // no distance (DAG prefetch reads DT_NONE: nothing to follow) and every code unresolved (K3)
+      HIPCHK(hipMemsetAsync(c->d_dt + (size_t)slot * c->tstride, 0xFF, c->tstride, c->s));
       HIPCHK(hipMemsetAsync(c->d_nh + (size_t)slot * c->tstride, 0xFF, c->tstride, c->s));
     }
     HIPCHK(hipMemsetAsync(&c->d_stat->err, 0, 4, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
+  }
+  return check_err(c);
+}
+
+// K1 of `goals` (host array) into u16 tables for an API that returns them: batches through the K1
+// buffer, each batch handed to `take(device tables, first goal index, count)` (the store holds detour
+// bytes only, tsw_internal.h).
+template <class Take>
+int build_u16(tsw_ctx* c, const uint32_t* goals, uint32_t k, Take&& take) {
+  size_t batch = 0;
+  TRY(ensure_ktmp(c, k, &batch));
+  TRY(ensure_tmp(c, std::min<size_t>(k, batch)));
+  for (uint32_t i0 = 0; i0 < k; i0 += (uint32_t)batch) {
+    const uint32_t nb = (uint32_t)std::min<size_t>(batch, k - i0);
+    // launch order longest-first (bfs_lpt_order); the slots carry each table's position in the batch
+    std::vector<uint32_t> bg(goals + i0, goals + i0 + nb), bs(nb);
+    for (uint32_t j = 0; j < nb; ++j) bs[j] = j;
+    bfs_lpt_order(c, bg, bs);
+    HIPCHK(hipMemcpyAsync(c->d_tmp_a, bg.data(), (size_t)nb * 4, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_tmp_b, bs.data(), (size_t)nb * 4, hipMemcpyHostToDevice, c->s));
+    TRY(run_bfs(c, c->d_tmp_a, c->d_tmp_b, nb, c->d_ktmp, c->tstride, nullptr));
+    TRY(take(c->d_ktmp, i0, nb));
+    HIPCHK(hipStreamSynchronize(c->s));  // the next batch reuses the buffer and the goal upload
   }
   return check_err(c);
 }
@@ -1285,7 +1344,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   P.ab_flags = c->tun.ab_flags;
   P.t0_delay_ticks = c->tun.t0_delay_us * 100u;
   P.prefetch_ext = c->tun.prefetch_ext;
-  P.dist = c->d_dist;
+  P.dt = c->d_dt;
   P.nbmask = c->d_nbmask;
   P.live = c->d_live;
   P.klt = c->d_klt;
@@ -1467,7 +1526,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     W.slow_mask = (1u << c->tun.slow_poll) - 1u;
     W.slow_mult = c->tun.slow_mult;
     W.idle_ticks = c->tun.worker_idle_us * 100ull;  // wall clock: 100 MHz
-    W.dist = c->d_dist;
+    W.dt = c->d_dt;
     W.gs_lds = wcfg.gs_lds;
     W.stage_fb = wcfg.stage_fb;
     W.hcap = wcfg.hcap;
@@ -2047,7 +2106,7 @@ void tsw_destroy(tsw_ctx* c) {
   auto fre = [](void* p) {
     if (p) (void)hipFree(p);
   };
-  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_frb); fre(c->d_abase); fre(c->d_wlg); fre(c->d_anch); fre(c->d_lovf); fre(c->d_bprof); fre(c->d_dist); fre(c->d_nh); fre(c->d_goal_tab);
+  fre(c->d_nbmask); fre(c->d_freebits); fre(c->d_frp); fre(c->d_frb); fre(c->d_abase); fre(c->d_wlg); fre(c->d_anch); fre(c->d_lovf); fre(c->d_bprof); fre(c->d_dt); fre(c->d_ktmp); fre(c->d_tmp_c); fre(c->d_nh); fre(c->d_goal_tab);
   fre(c->d_heaps); fre(c->d_gs); fre(c->d_epochs); fre(c->d_Q); fre(c->d_res); fre(c->d_lens);
   fre(c->d_gs16); fre(c->d_ep16); fre(c->d_ovf); fre(c->d_ovf2);
   fre(c->d_stat); fre(c->d_v); fre(c->d_g); fre(c->d_cnt); fre(c->d_succ); fre(c->d_ap); fre(c->d_st);
@@ -2382,12 +2441,12 @@ int tsw_dist_tables(tsw_ctx* c, const uint32_t* goals, uint32_t k, uint16_t* out
   TRY(ensure_tables(c, gv));
   TRY(require_real_tables(c, gv));
   const size_t ncell = c->G.ncell;
-  for (uint32_t i = 0; i < k; ++i) {
-    const int32_t slot = c->h_goal_tab[gv[i]];
-    HIPCHK(hipMemcpyAsync(out + (size_t)i * ncell, c->d_dist + (size_t)slot * c->tstride, ncell * 2,
-                          hipMemcpyDeviceToHost, c->s));
-  }
-  HIPCHK(hipStreamSynchronize(c->s));
+  TRY(build_u16(c, gv.data(), k, [&](const uint16_t* d, uint32_t i0, uint32_t nb) -> int {
+    for (uint32_t j = 0; j < nb; ++j)
+      HIPCHK(hipMemcpyAsync(out + (size_t)(i0 + j) * ncell, d + (size_t)j * c->tstride, ncell * 2,
+                            hipMemcpyDeviceToHost, c->s));
+    return TSW_OK;
+  }));
   resolve_timing(c);
   return TSW_OK;
 }
@@ -2437,15 +2496,13 @@ int tsw_import_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, cons
   auto ingest = [&]() -> int {
     TRY(reserve_slots(c, newg.size(), slots));
     for (uint32_t sl : slots) c->h_tab_tableless[sl] = 0;  // imported: real u16 tables
-    const size_t ncell = c->G.ncell;
-    for (size_t j = 0; j < newg.size(); ++j)
-      HIPCHK(hipMemcpyAsync(c->d_dist + (size_t)slots[j] * c->tstride, dev_tables + (size_t)src[j] * ncell,
-                            ncell * 2, hipMemcpyDeviceToDevice, c->s));
     TRY(ensure_tmp(c, newg.size()));
     HIPCHK(hipMemcpyAsync(c->d_tmp_a, newg.data(), newg.size() * 4, hipMemcpyHostToDevice, c->s));
     HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
-    HIPCHK(launch_classify(c->G, c->d_tmp_a, c->d_tmp_b, (uint32_t)newg.size(), c->d_dist, c->tstride, c->d_nh,
-                           c->s));
+    HIPCHK(hipMemcpyAsync(c->d_tmp_c, src.data(), src.size() * 4, hipMemcpyHostToDevice, c->s));
+    // codes and detour bytes straight from the caller's u16 tables (the store keeps no u16 copy)
+    HIPCHK(launch_classify_dt(c->G, c->d_tmp_a, c->d_tmp_c, c->d_tmp_b, (uint32_t)newg.size(), dev_tables,
+                              c->G.ncell, c->d_nh, c->d_dt, c->tstride, c->s));
     HIPCHK(hipStreamSynchronize(c->s));
     return TSW_OK;
   };
@@ -2505,12 +2562,15 @@ int tsw_next_hop_tables_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, ui
     const int32_t slot = c->h_goal_tab[gv[i]];
     HIPCHK(hipMemcpyAsync(dev_out + (size_t)i * ncell, c->d_nh + (size_t)slot * c->tstride, ncell,
                           hipMemcpyDeviceToDevice, c->s));
-    // the K1 tables the codes were resolved from, out of the store (one K1 build serves both
-    // all-gathers of a shard: ADVICE r2)
-    if (dev_dist)
-      HIPCHK(hipMemcpyAsync(dev_dist + (size_t)i * ncell, c->d_dist + (size_t)slot * c->tstride, ncell * 2,
-                            hipMemcpyDeviceToDevice, c->s));
   }
+  // the u16 K1 tables beside the codes (the store holds detour bytes only: K1 again, into the caller's buffer)
+  if (dev_dist)
+    TRY(build_u16(c, gv.data(), k, [&](const uint16_t* d, uint32_t i0, uint32_t nb) -> int {
+      for (uint32_t j = 0; j < nb; ++j)
+        HIPCHK(hipMemcpyAsync(dev_dist + (size_t)(i0 + j) * ncell, d + (size_t)j * c->tstride, ncell * 2,
+                              hipMemcpyDeviceToDevice, c->s));
+      return TSW_OK;
+    }));
   HIPCHK(hipStreamSynchronize(c->s));
   resolve_timing(c);
   return TSW_OK;
@@ -2533,12 +2593,16 @@ int tsw_import_next_hops_device(tsw_ctx* c, const uint32_t* goals, uint32_t k, c
     TRY(reserve_slots(c, newg.size(), slots));
     for (uint32_t sl : slots) c->h_tab_tableless[sl] = 0;  // imported: real u16 tables
     const size_t ncell = c->G.ncell;
-    for (size_t j = 0; j < newg.size(); ++j) {
-      HIPCHK(hipMemcpyAsync(c->d_dist + (size_t)slots[j] * c->tstride, dev_dist + (size_t)src[j] * ncell,
-                            ncell * 2, hipMemcpyDeviceToDevice, c->s));
+    for (size_t j = 0; j < newg.size(); ++j)
       HIPCHK(hipMemcpyAsync(c->d_nh + (size_t)slots[j] * c->tstride, dev_nh + (size_t)src[j] * ncell, ncell,
                             hipMemcpyDeviceToDevice, c->s));
-    }
+    // detour bytes from the u16 tables (the imported codes stay: nh = null)
+    TRY(ensure_tmp(c, newg.size()));
+    HIPCHK(hipMemcpyAsync(c->d_tmp_a, newg.data(), newg.size() * 4, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_tmp_b, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, c->s));
+    HIPCHK(hipMemcpyAsync(c->d_tmp_c, src.data(), src.size() * 4, hipMemcpyHostToDevice, c->s));
+    HIPCHK(launch_classify_dt(c->G, c->d_tmp_a, c->d_tmp_c, c->d_tmp_b, (uint32_t)newg.size(), dev_dist, ncell,
+                              nullptr, c->d_dt, c->tstride, c->s));
     // a pending marker from the producing context means "not resolved": unknown here — swept over
     // the imported slots only (a whole-store sweep grows with every table the context holds)
     for (size_t j = 0; j < newg.size(); ++j)

@@ -5,8 +5,10 @@
 //   nbmask  [ncell]            u8   bit d (0..3) = neighbour in dir d exists
 //                                   (S,E,N,W: tswap.rs:62), bit 7 = free cell
 //   freebits[H*Ww]             u32  row-major bitmap of free cells, Ww = ceil(W/32)
-//   dist    [cap][tstride]     u16  K1 BFS table per goal (TSW_DIST_INF = blocked /
-//                                   unreachable), tstride = round_up(ncell, 8)
+//   dt      [cap][tstride]     u8   detour byte per (goal, cell): min((D - |c - goal|_1) / 2, 255),
+//                                   D = the K1 BFS distance; 255 = blocked / unreachable / detour
+//                                   >= 510 (round 6: the u16 table D is built per batch, classified
+//                                   and dropped), tstride = round_up(ncell, 8)
 //   nh      [cap][tstride]     u8   next-hop code per (goal, cell): 0..3 = move in
 //                                   dir d, 4 = stay (fallback with no closer
 //                                   neighbour), NH_UNKNOWN = needs exact A*
@@ -33,6 +35,7 @@ constexpr uint8_t NH_PENDING_S = 0xFD;  // queued speculatively for the concurre
 constexpr uint8_t NH_PENDING = 0xFE;    // queued for a K3 pass (needed)
 constexpr uint8_t NH_UNKNOWN = 0xFF;
 constexpr uint16_t DIST_INF = 0xFFFF;
+constexpr uint8_t DT_NONE = 0xFF;  // detour byte: blocked / unreachable / saturated
 constexpr uint8_t NB_FREE = 0x80;
 
 // internal agent states (tswap.rs:84-88)
@@ -53,7 +56,7 @@ struct DevGrid {
 };
 
 struct Tables {
-  uint16_t* dist;
+  uint8_t* dt;
   uint8_t* nh;
   int32_t* goal_tab;
   uint32_t* tab_goal;

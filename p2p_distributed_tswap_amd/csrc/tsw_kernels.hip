@@ -562,6 +562,56 @@ hipError_t launch_bfs(const DevGrid& G, const uint32_t* goals, const uint32_t* s
   return hipGetLastError();
 }
 
+// The table store's format (round 6): per goal, u8 next-hop codes and u8 detour bytes
+// DT[c] = min((D[c] - |c - goal|_1) / 2, 255), 255 also for blocked / unreachable cells (D and the
+// Manhattan distance share parity on a 4-grid). A goal's u16 table D (index src[i], or i, of `dist`)
+// goes into store slot slots[i]: codes (nh_base, unless null: imported codes are kept) and detour bytes.
+__global__ void k_classify_dt(DevGrid G, const uint32_t* __restrict__ goals, const uint32_t* __restrict__ src,
+                              const uint32_t* __restrict__ slots, uint32_t k, const uint16_t* __restrict__ dist,
+                              uint64_t dstride, uint8_t* __restrict__ nh_base, uint8_t* __restrict__ dt_base,
+                              uint64_t tstride) {
+  const uint32_t ncp8 = (G.ncell + 7u) / 8u;
+  const uint64_t total = (uint64_t)k * ncp8;
+  for (uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t gi = (uint32_t)(idx / ncp8), c8 = (uint32_t)(idx % ncp8);
+    const uint32_t goal = goals[gi];
+    const uint64_t slot = slots[gi];
+    const uint16_t* D = dist + (uint64_t)(src ? src[gi] : gi) * dstride;
+    const uint32_t gx = goal % G.W, gy = goal / G.W;
+    const uint64_t m8 = reinterpret_cast<const uint64_t*>(G.nbmask)[c8];
+    uint64_t codes = 0, dts = 0;
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t c = c8 * 8u + j;
+      uint8_t code = NH_UNKNOWN, db = DT_NONE;
+      if (c < G.ncell) {
+        if (nh_base) code = classify_cell(D, c, (uint8_t)(m8 >> (8 * j)), G.W, goal, gx, gy);
+        const uint32_t d = D[c];
+        if (d != DIST_INF) {
+          const uint32_t y = c / G.W, x = c - y * G.W;
+          const uint32_t man = (x > gx ? x - gx : gx - x) + (y > gy ? y - gy : gy - y);
+          db = d < man ? DT_NONE : (uint8_t)min((d - man) >> 1, (uint32_t)DT_NONE);
+        }
+      }
+      codes |= (uint64_t)code << (8 * j);
+      dts |= (uint64_t)db << (8 * j);
+    }
+    if (nh_base) reinterpret_cast<uint64_t*>(nh_base + slot * tstride)[c8] = codes;
+    reinterpret_cast<uint64_t*>(dt_base + slot * tstride)[c8] = dts;
+  }
+}
+
+hipError_t launch_classify_dt(const DevGrid& G, const uint32_t* goals, const uint32_t* src, const uint32_t* slots,
+                              uint32_t k, const uint16_t* dist, uint64_t dstride, uint8_t* nh_base, uint8_t* dt_base,
+                              uint64_t tstride, hipStream_t s) {
+  if (k == 0) return hipSuccess;
+  const uint64_t total = (uint64_t)k * ((G.ncell + 7u) / 8u);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((total + 255) / 256, 65535);
+  hipLaunchKernelGGL(k_classify_dt, dim3(grid), dim3(256), 0, s, G, goals, src, slots, k, dist, dstride, nh_base,
+                     dt_base, tstride);
+  return hipGetLastError();
+}
+
 hipError_t launch_classify(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                            const uint16_t* dist_base, uint64_t stride, uint8_t* nh_base, hipStream_t s) {
   if (k == 0) return hipSuccess;

@@ -122,6 +122,10 @@ hipError_t launch_bfs_mg(const MgBfsArgs& A, int max_lds, int num_cu, hipStream_
 
 hipError_t launch_classify(const DevGrid& G, const uint32_t* goals, const uint32_t* slots, uint32_t k,
                            const uint16_t* dist_base, uint64_t stride, uint8_t* nh_base, hipStream_t s);
+// store slots[i] <- codes (nh_base != null) + detour bytes of the u16 table src[i] (or i) of `dist`
+hipError_t launch_classify_dt(const DevGrid& G, const uint32_t* goals, const uint32_t* src, const uint32_t* slots,
+                              uint32_t k, const uint16_t* dist, uint64_t dstride, uint8_t* nh_base, uint8_t* dt_base,
+                              uint64_t tstride, hipStream_t s);
 
 hipError_t launch_astar(const DevGrid& G, const AstarQuery* Q, const uint32_t* nq_dev, uint32_t nq_host,
                         uint32_t launch_threads, uint8_t* nh_base, uint64_t nstride, uint8_t* res,

@@ -66,7 +66,7 @@ struct PlanArgs {
   uint32_t ab_flags;            // diagnostic A/B switches (Tunables::ab_flags; 0 in the product build)
   uint32_t t0_delay_ticks;      // diagnostic: idle after step 0's assignment (100 MHz ticks)
   uint32_t prefetch_ext;        // bit 0: DAG from an agent's own unresolved cell; bit 1: walk on past the pickup
-  const uint16_t* dist;         // K1 distance tables (nstride entries per slot), for dag_prefetch
+  const uint8_t* dt;            // detour bytes of the table store (nstride per slot; tsw_internal.h), for dag_prefetch
   const uint8_t* nbmask;        // per cell: bit d = neighbour in direction d is free
   uint32_t* v;
   uint32_t* g;
@@ -179,9 +179,9 @@ struct WorkerArgs {
   uint32_t lds_per_wave;
   uint32_t nworkers;   // worker waves in the dispatch (<= the global g-score / heap slots)
   // exact DAG early exit of the A* (tsw_astar.h): 0 off, 1 the goal's detour bytes staged in this
-  // wave's LDS (after the free bitmap), 2 the goal's u16 table read from global memory
+  // wave's LDS (after the free bitmap), 2 the goal's detour bytes read from the table store
   uint32_t dag;
-  const uint16_t* dist;  // K1 tables, nstride entries per goal slot
+  const uint8_t* dt;     // detour bytes of the table store, nstride per goal slot
   uint32_t dag_mask;     // the DAG test runs when (pops & dag_mask) == 0
   uint32_t stale_steps;  // speculative entries queued more than this many timesteps ago are dropped (0: never)
   uint32_t reg_heap;     // A* heaps up to this many entries live in registers (0: LDS array only; <= 63)

@@ -638,8 +638,17 @@ __device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t
 __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint32_t g, int32_t tab) {
   constexpr uint32_t DAG_WIDTH = 16;  // array bound; P.dag_width caps the frontier (default 4)
   const uint32_t dwid = P.dag_width ? min(P.dag_width, DAG_WIDTH) : 4u;
-  const uint16_t* dt = P.dist + (uint64_t)tab * P.nstride;
+  const uint8_t* dtb = P.dt + (uint64_t)tab * P.nstride;
   const uint8_t* ht = P.nh + (uint64_t)tab * P.nstride;
+  const uint32_t gy = g / P.W, gx = g - gy * P.W;
+  // K1 distance from the detour byte: |c - g|_1 + 2 * detour, ~0 when unknown (blocked / unreachable /
+  // saturated: the speculative walk stops there)
+  auto dist_of = [&](uint32_t c) -> uint32_t {
+    const uint32_t b = dtb[c];
+    if (b == DT_NONE) return 0xFFFFFFFFu;
+    const uint32_t y = c / P.W, x = c - y * P.W;
+    return (x > gx ? x - gx : gx - x) + (y > gy ? y - gy : gy - y) + 2u * b;
+  };
   uint32_t fr[DAG_WIDTH], nf = 1;
   fr[0] = u;
   for (uint32_t lv = 0; lv < P.dag_prefetch && nf > 0u; ++lv) {
@@ -658,13 +667,14 @@ __device__ void dag_prefetch(const PlanArgs& P, uint32_t* s_q, uint32_t u, uint3
         continue;
       }
       if (cx == NH_STAY) continue;
-      const uint32_t dx = dt[x];
+      const uint32_t dx = dist_of(x);
+      if (dx == 0xFFFFFFFFu) continue;
       const uint8_t nb = P.nbmask[x];
 #pragma unroll
       for (uint32_t d = 0; d < 4u; ++d) {
         if (!((nb >> d) & 1u)) continue;
         const uint32_t w = step_cell(x, d, P.W);
-        if (w == g || (uint32_t)dt[w] + 1u != dx) continue;
+        if (w == g || dist_of(w) + 1u != dx) continue;
         if (ht[w] == NH_UNKNOWN) prefetch_pair(P, w, g, tab, s_q);
         add(w);
       }

@@ -239,23 +239,22 @@ __device__ __forceinline__ void coop_worker(const WorkerArgs& A, uint64_t* wsm, 
     uint8_t code = NH_UNKNOWN;
     uint32_t np = 0, npt = 0;  // heap pops (diagnostics)
     uint32_t dag = tab >= 0 ? A.dag : 0u;
-    const uint16_t* DGt = dag ? A.dist + (uint64_t)tab * A.nstride : nullptr;
+    const uint8_t* DGt = dag ? A.dt + (uint64_t)tab * A.nstride : nullptr;
     if (dag == 1u) {
-      // the query's ellipse box: d* = D[v], margin (d* - |v - goal|) / 2 around the start/goal box
+      // the query's ellipse box: d* = |v - goal| + 2 * detour(v), margin detour(v) around the start/goal box
       const uint32_t W = G.W, vy = v / W, vx = v - vy * W, gy = goal / W, gx = goal - gy * W;
-      const uint32_t ds = __builtin_amdgcn_readfirstlane((uint32_t)DGt[v]);
-      const uint32_t man = (vx > gx ? vx - gx : gx - vx) + (vy > gy ? vy - gy : gy - vy);
-      if (ds == 0xFFFFu || ds > 508u || ds < man) {
+      const uint32_t dv = __builtin_amdgcn_readfirstlane((uint32_t)DGt[v]);
+      if (dv == DT_NONE) {
         dag = 0u;  // unreachable or detour past the byte range: the full search
       } else {
-        const uint32_t e = (ds - man) >> 1;
+        const uint32_t e = dv;
         const uint32_t x0 = min(vx, gx) > e ? min(vx, gx) - e : 0u, x1 = min(max(vx, gx) + e, W - 1u);
         const uint32_t y0 = min(vy, gy) > e ? min(vy, gy) - e : 0u, y1 = min(max(vy, gy) + e, G.H - 1u);
         const bool inside = dt_goal == goal && x0 >= (dt_bx & 0xFFFFu) && x1 <= (dt_bx >> 16) &&
                             y0 >= (dt_by & 0xFFFFu) && y1 <= (dt_by >> 16);
         if (!inside) {
           const unsigned long long ts0 = wall_clock64();
-          stage_detour(DT, DGt, W, goal, x0, x1, y0, y1, lane);
+          stage_detour(DT, DGt, W, x0, x1, y0, y1, lane);
           dt_goal = goal;
           dt_bx = x0 | (x1 << 16);
           dt_by = y0 | (y1 << 16);

@@ -1,6 +1,7 @@
 """Per-context HBM: device memory a planner context holds after one full-horizon plan of each config
 (free device memory before the context is created minus free memory after the plan, the context still
-open), split into the table store (u16 distance tables + u8 next-hop codes, from the context's stats)
+open), split into the table store (u8 detour bytes + u8 next-hop codes per goal table since round 6; u16
+distances + codes before, from the context's stats)
 and everything else (K3 scratch slots, coop queues, records, agent/task state, K1 scratch).
 
 usage: python scripts/ctx_hbm.py [config ...]   (default: the three BASELINE planning configs)
@@ -37,7 +38,7 @@ def main():
             st = p.stats()
             tables = int(st["tables"])
             ncell = len(rows) * len(rows[0])
-            store = tables * ncell * 3  # u16 distances + u8 codes per goal table
+            store = tables * ncell * 2  # u8 detour bytes + u8 codes per goal table (round 6)
             print(json.dumps({
                 "config": name, "agents": len(starts), "tasks": len(tasks), "cells": ncell,
                 "timesteps": int(rec.shape[1]), "tables": tables,

@@ -25,7 +25,7 @@ def test_step_streams_goals_through_small_budget():
     rows = maps.random_map(32, 32, 0.20, 0x3232)
     cells, cid = _cells(rows)
     og = OracleGraph(cells)
-    per_table = ((32 * 32 + 7) // 8 * 8) * 3
+    per_table = ((32 * 32 + 7) // 8 * 8) * 2  # detour byte + next-hop code per cell (round 6)
     rng = np.random.default_rng(21)
     n = 20
     v = cid[rng.choice(cid.size, n, replace=False)]
@@ -46,7 +46,7 @@ def test_budget_too_small_for_one_call_then_recovers():
     rows = maps.random_map(32, 32, 0.20, 0x3232)
     cells, cid = _cells(rows)
     og = OracleGraph(cells)
-    per_table = ((32 * 32 + 7) // 8 * 8) * 3
+    per_table = ((32 * 32 + 7) // 8 * 8) * 2  # detour byte + next-hop code per cell (round 6)
     goals = cid[:40]
     with Planner(rows, table_budget_bytes=16 * per_table) as p:
         with pytest.raises(TswapError) as ei:
