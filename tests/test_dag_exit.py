@@ -101,3 +101,62 @@ def test_dag_exit_matches_full_astar(name, rows):
         total += p_full
     assert total > 0
     print(f"{name}: DAG early exit saves {saved / total:.1%} of {total} pops")
+
+
+def detour_bytes(D, W, goal, cap=255):
+    """The table store's detour bytes (round 6, tsw_internal.h): min((D - |c - goal|_1) / 2, cap), cap for
+    unreachable cells. `cap` below 255 makes saturation common on small maps."""
+    gx, gy = goal % W, goal // W
+    c = np.arange(D.size)
+    man = np.abs(c % W - gx) + np.abs(c // W - gy)
+    det = (D.astype(np.int64) - man) // 2
+    return np.where(D == INF, cap, np.minimum(det, cap)).astype(np.int64)
+
+
+def astar_dag_exit_bytes(W, H, free, D, v, goal, cap):
+    """astar_dag_exit with the workers' byte test: d* = h(v) + 2 b(v) (no early exit when b(v) == cap) and
+    a node is a DAG node iff b(n) != cap and g + h(n) + 2 b(n) == d* (tsw_astar.h)."""
+    b = detour_bytes(D, W, goal, cap)
+    gx, gy = goal % W, goal // W
+    h = lambda c: abs(c % W - gx) + abs(c // W - gy)  # noqa: E731
+    if b[v] == cap:
+        return None
+    Dx = np.where(b == cap, INF, np.array([h(c) for c in range(D.size)]) + 2 * b)  # INF never matches
+    assert Dx[v] == D[v]
+    return astar_dag_exit(W, H, free, Dx, v, goal)
+
+
+@pytest.mark.parametrize("cap", [2, 6, 255])
+def test_dag_exit_with_saturated_detour_bytes(cap):
+    """The byte form of the test is exact even when bytes saturate: along a shortest path toward the goal D
+    drops by 1 per hop and the Manhattan distance by at most 1, so the detour never grows, and every DAG node
+    of a query has detour <= detour(start) < cap — skipping saturated cells skips no DAG node."""
+    rows = maps.cave_map(40, 41, 3)
+    checked = 0
+    for (W, H, free, D, og, v, g) in _pairs(rows, 300, 0xB17E):
+        r = astar_dag_exit_bytes(W, H, free, D, v, g, cap)
+        if r is None:
+            continue
+        lab, _, _ = r
+        dx, dy = DIRS[lab]
+        assert og.get_path_next(v, g)[0] == (v // W + dy) * W + v % W + dx, (cap, v, g)
+        checked += 1
+    assert checked > 0
+
+
+def test_detour_never_grows_along_shortest_paths():
+    rows = maps.cave_map(40, 41, 3)
+    arr = maps.rows_to_array(rows)
+    H, W = arr.shape
+    free = arr.reshape(-1) != ord("@")
+    og = OracleGraph(arr)
+    rng = np.random.default_rng(0xDE70)
+    for g in rng.choice(np.flatnonzero(free), 12, replace=False):
+        D = og.bfs(int(g)).reshape(-1).astype(np.int64)
+        det = detour_bytes(D, W, int(g), cap=1 << 30)
+        for c in np.flatnonzero((D != INF) & free):
+            cx, cy = c % W, c // W
+            for dx, dy in DIRS:
+                nx, ny = cx + dx, cy + dy
+                if 0 <= nx < W and 0 <= ny < H and free[ny * W + nx] and D[ny * W + nx] == D[c] - 1:
+                    assert det[ny * W + nx] <= det[c]
