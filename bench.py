@@ -493,8 +493,17 @@ def main():
         cst = cp.stats()
         k_ms = cst["bfs_ms"] / max(cst["bfs_launches"], 1)
         bytes_goal = bfs_bytes_per_goal(256, 257, False)
-        gather_ms = None
+        gather_ms = local_ms = None
         if dist is not None:
+            # the alternative the sharded build competes with: every rank builds all the
+            # goals' tables itself, no collective (wall time, max over ranks)
+            allout = torch.empty((goals.size, ncell), dtype=torch.int16, device="cuda")
+            barrier()
+            tl = time.perf_counter()
+            cp.dist_tables_device(goals, allout.data_ptr())
+            barrier()
+            local_ms = allmax(time.perf_counter() - tl) * 1e3
+            del allout
             # goal-sharded K1 + RCCL all-gather over xGMI (north_star), then every rank ingests
             # every table into its table store (sharding.py)
             from p2p_distributed_tswap_amd import sharding
@@ -539,6 +548,8 @@ def main():
             },
             # N > 1: wall time of (this rank's K1 shard + RCCL all-gather of all tables), max over ranks
             "sharded_build_allgather_ms": round(gather_ms, 3) if gather_ms is not None else None,
+            # ... and the same N ranks each building all goals locally (the sharded form pays iff smaller)
+            "local_build_all_goals_ms": round(local_ms, 3) if local_ms is not None else None,
         }
         del out
         cp.close()
