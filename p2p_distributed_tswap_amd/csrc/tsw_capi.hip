@@ -66,6 +66,7 @@ struct Tunables {
   uint32_t astar_diag = 0;        // TSW_ASTAR_SERIAL / TSW_ASTAR_PROF (ASTAR_DIAG_*)
   bool prefetch = true;           // TSW_NO_PREFETCH: no speculative next-hop prefetch
   uint32_t wave_rules_max = 0xFFFFFFFFu;  // TSW_WAVE_RULES_MAX: wave-0 rules rounds when n <= this
+  uint32_t walk_cap = 16;  // TSW_WALK_CAP: successor-walk hops of a batched rules firing (longer ones fire alone)
   uint32_t wide_prefetch = 8;     // TSW_WIDE_PREFETCH: resolved hops walked ahead (0 = candidates only)
   uint32_t wide_hi = 32, wide_lo = 8;  // TSW_WIDE_HI / TSW_WIDE_LO: coop step-start walk-ahead hops (grids <= 2^18 cells with a small backlog / grids > 2^18 cells); round 5, busy instances: 16 -> 32 and 4 -> 8 (profiles/r5/retune_busy_ab.txt)
   bool hot_chains = true;         // TSW_HOT_CHAINS=0: no planner-fed chains of just-assigned tasks (A/B)
@@ -126,6 +127,7 @@ struct Tunables {
     t.astar_diag = (getenv("TSW_ASTAR_SERIAL") ? ASTAR_DIAG_SERIAL : 0u) | (getenv("TSW_ASTAR_PROF") ? ASTAR_DIAG_PROF : 0u);
     t.prefetch = getenv("TSW_NO_PREFETCH") == nullptr;
     t.wave_rules_max = (uint32_t)num("TSW_WAVE_RULES_MAX", 0, 0xFFFFFFFFl, t.wave_rules_max);
+    t.walk_cap = (uint32_t)num("TSW_WALK_CAP", 0, 4096, t.walk_cap);
     t.wide_prefetch = (uint32_t)num("TSW_WIDE_PREFETCH", 0, 1 << 16, t.wide_prefetch);
     t.wide_hi = (uint32_t)num("TSW_WIDE_HI", 0, 1 << 16, t.wide_hi);
     t.wide_lo = (uint32_t)num("TSW_WIDE_LO", 1, 1 << 16, t.wide_lo);
@@ -261,7 +263,7 @@ struct tsw_ctx {
   size_t predcap = 0;
   size_t qtcap = 0;
   uint32_t qt_count = 0;
-  uint32_t* h_flags = nullptr;   // pinned, coherent: [0] planner resident, [1] abort, [2] heartbeat
+  uint32_t* h_flags = nullptr;   // pinned, coherent: [0] planner resident, [1] abort, [2] heartbeat, [8..23] PBAR
   uint32_t* d_flags = nullptr;
   uint64_t coop_aborts = 0;
   uint32_t watchdog_ms = 10000;  // tsw_opts.watchdog_ms
@@ -272,8 +274,8 @@ struct tsw_ctx {
   DevStatus* d_stat = nullptr;
   DevStatus* h_stat = nullptr;   // pinned, D2H
   PlanCtl* d_ctl = nullptr;
-  PlanArgs* d_pargs = nullptr;  // k_plan reads its arguments from here
   PlanCtl* h_ctl = nullptr;      // pinned
+  PlanArgs* d_pargs = nullptr;  // k_plan reads its arguments from here
   unsigned long long* d_ticks = nullptr;
   uint32_t* d_dtag = nullptr;  // TSW_PLAN_DEBUG: per-agent change tags (PlanArgs::dtag)
   uint32_t dtag_cap = 0;
@@ -1334,6 +1336,7 @@ PlanArgs plan_args(tsw_ctx* c, uint32_t n, uint32_t m, uint32_t mode, bool want_
   // agents are dense, so a scan rarely needs more than a chunk or two even for 10k agents;
   // TSW_WAVE_RULES_MAX caps n for A/B
   P.wave_rules_max = c->tun.wave_rules_max;
+  P.walk_cap = c->tun.walk_cap;
   P.wide_prefetch = c->tun.wide_prefetch;
   P.wide_hi = c->tun.wide_hi ? c->tun.wide_hi : c->tun.wide_prefetch;
   P.wide_lo = c->tun.wide_lo;
@@ -1567,6 +1570,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       hf[0] = 0u;
       hf[1] = 0u;
       hf[2] = 0u;
+      for (int w = 4; w < 40; ++w) hf[w] = 0u;  // barrier breadcrumbs (TSW_PLAN_DEBUG)
     }
     {
       Timer t(c, CAT_WALK);
@@ -1601,6 +1605,13 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
           if (c->watchdog_ms >= 1000u)
             fprintf(stderr, "[tswap] watchdog: planner made no step for %u ms; finishing the call in exit mode\n",
                     c->watchdog_ms);
+          if (c->tun.plan_debug && hf[24]) {  // per-wave barrier breadcrumbs (-DTSW_PBAR): line | 0x10000 once passed
+            fprintf(stderr, "[tswap] planner waves at barriers:");
+            for (int w = 0; w < 16; ++w) fprintf(stderr, " %u%s", hf[8 + w] & 0xFFFFu, (hf[8 + w] >> 16) ? "+" : "");
+            fprintf(stderr, "\n[tswap] barriers passed per wave:");
+            for (int w = 0; w < 16; ++w) fprintf(stderr, " %u", hf[24 + w]);
+            fprintf(stderr, "\n[tswap] first mismatch: wave 0 at %u, another at %u\n", hf[4] >> 16, hf[4] & 0xFFFFu);
+          }
         }
         std::this_thread::sleep_for(std::chrono::microseconds(50));
       }
@@ -1635,7 +1646,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
     const PlanCtl& k = *c->h_ctl;
     if (k.err & ERR_ABORT) {
       if (c->tun.plan_debug) {  // diagnostics: where the stopped planner spent its time (section / sub-phase ticks)
-        unsigned long long tk[40];
+        unsigned long long tk[48];
         if (hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost) == hipSuccess) {
           std::string line = "[k_plan] watchdog stop, ticks:";
           for (int q = 0; q < 40; ++q) line += " " + std::to_string(q) + ":" + std::to_string(tk[q]);
@@ -1664,7 +1675,7 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
       c->st.rule_rounds += k.rule_rounds;
       c->st.move_rounds += k.move_rounds;
       if (c->tun.plan_debug) {
-        unsigned long long tk[40];
+        unsigned long long tk[48];
         HIPCHK(hipMemcpy(tk, c->d_ticks, sizeof tk, hipMemcpyDeviceToHost));
         fprintf(stderr, "[k_plan] assign us: transitions %.0f compaction %.0f scan %.0f accept %.0f update %.0f | sections %llu batches %llu accepted %llu\n",
                 tk[32] / 100.0, tk[33] / 100.0, tk[34] / 100.0, tk[35] / 100.0, tk[36] / 100.0, tk[39], tk[37], tk[38]);
@@ -1674,6 +1685,8 @@ int run_plan_impl(tsw_ctx* c, PlanArgs& P, const PlanCtl& init) {
                 "loads %llu fast firings %llu | rotations %llu, settle kcycles: successors %.0f walk %.0f\n",
                 tk[16] / 1e3, tk[17] / 1e3, tk[18] / 1e3, tk[19] / 1e3, tk[20] / 1e3, tk[21] / 1e3, tk[22], tk[23],
                 tk[11], tk[30] / 1e3, tk[31] / 1e3);
+        fprintf(stderr, "[k_plan] wave rules batches %llu (longest walks %llu hops) kcycles: marks %.0f walks %.0f apply %.0f\n",
+                tk[43], tk[44], tk[40] / 1e3, tk[41] / 1e3, tk[42] / 1e3);
         fprintf(stderr, "[k_plan] steps %u rule rounds %u move rounds %u launches %llu | move A-E us %.0f %.0f %.0f %.0f %.0f"
                 " | rules scan %.0f fire %.0f relabel %.0f\n", k.steps_run, k.rule_rounds, k.move_rounds,
                 (unsigned long long)round + 1ull, tk[8] / 100.0, tk[9] / 100.0, tk[10] / 100.0, tk[11] / 100.0,
@@ -2080,14 +2093,14 @@ tsw_ctx* tsw_create(const uint8_t* cells, uint32_t w, uint32_t h, const tsw_opts
     return fail("pinned status", e);
   if ((e = hipMalloc(&c->d_ctl, sizeof(PlanCtl))) != hipSuccess) return fail("malloc ctl", e);
   if ((e = hipMalloc(&c->d_pargs, sizeof(PlanArgs))) != hipSuccess) return fail("malloc plan args", e);
-  if ((e = hipMalloc(&c->d_ticks, 40 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
-  if ((e = hipMemsetAsync(c->d_ticks, 0, 40 * sizeof(unsigned long long), c->s)) != hipSuccess)
+  if ((e = hipMalloc(&c->d_ticks, 48 * sizeof(unsigned long long))) != hipSuccess) return fail("malloc ticks", e);
+  if ((e = hipMemsetAsync(c->d_ticks, 0, 48 * sizeof(unsigned long long), c->s)) != hipSuccess)
     return fail("memset ticks", e);
   hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, c->device);
   if (c->wall_khz <= 0) c->wall_khz = 100000;
   if ((e = hipHostMalloc(&c->h_ctl, sizeof(PlanCtl), hipHostMallocDefault)) != hipSuccess)
     return fail("pinned ctl", e);
-  if ((e = hipHostMalloc(&c->h_flags, 16, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
+  if ((e = hipHostMalloc(&c->h_flags, 256, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
     return fail("pinned flags", e);
   if ((e = hipHostGetDevicePointer((void**)&c->d_flags, c->h_flags, 0)) != hipSuccess)
     return fail("flags device pointer", e);
@@ -2652,7 +2665,7 @@ int tsw_reset_stats(tsw_ctx* c) {
   const uint64_t tabs = c->st.tables;
   c->st = tsw_stats{};
   c->st.tables = tabs;
-  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 40 * sizeof(unsigned long long), c->s);
+  if (c->d_ticks) (void)hipMemsetAsync(c->d_ticks, 0, 48 * sizeof(unsigned long long), c->s);
   return TSW_OK;
 }
 

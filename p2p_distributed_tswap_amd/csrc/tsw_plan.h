@@ -57,6 +57,7 @@ struct PlanArgs {
   uint32_t mu_lds;              // occ_lds and the movement rounds' MU words in LDS too
   uint32_t part_lds;            // !agents_lds: PART_* agent arrays carved in LDS anyway (flat accesses)
   uint32_t wave_rules_max;      // rules rounds run in wave 0 alone when n <= this
+  uint32_t walk_cap;            // wave rules batches: longest successor walk a batched firing may take
   uint32_t wide_prefetch;       // 0: off; else also (succ cell, goal) of every agent, path walked this many hops ahead
   uint32_t wide_hi, wide_lo;    // coop mode: step-start walk-ahead hops when the speculative backlog is small / large
   uint32_t spec_hi;             // coop mode: backlog (queued, unclaimed speculative pairs) counted as small up to this
@@ -103,7 +104,7 @@ struct PlanArgs {
   uint64_t* rec;
   uint32_t* grec;
   PlanCtl* ctl;
-  unsigned long long* sec_ticks;  // [16] wall-clock ticks per section [0..7] and sub-phase [8..15] (diagnostics)
+  unsigned long long* sec_ticks;  // [48] wall-clock ticks per section [0..7], sub-phase ticks and counters [8..47] (diagnostics)
   uint32_t dbg;                   // sub-phase ticks on (TSW_PLAN_DEBUG)
   uint32_t* dtag;                 // diagnostics (TSW_PLAN_DEBUG): per agent, what changed it since PRE1 (CoopCtl::dbg_tag)
   // coop mode: K3 runs concurrently in the dispatch's worker workgroups (tsw_worker.h); Q is the needed queue (qcap entries for the

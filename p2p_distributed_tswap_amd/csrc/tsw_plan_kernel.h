@@ -43,10 +43,56 @@
 // whenever an instrumentation branch ran, and in a two-process run without them;
 // scripts/exp_lib.sh + hang_probe.py reproduce it.
 #define PLAN_DBG (P.dbg != 0u)
+// Planner barrier. Built with -DTSW_PBAR (scripts/exp_lib.sh) and run with TSW_PLAN_DEBUG, every barrier
+// also leaves per-wave breadcrumbs in the host-visible watchdog words (line reached / passed, barriers
+// passed: the watchdog prints them) and checks that all waves arrived at the same one. Round 6: this is
+// how the debug-mode hang was read — waves 1-15 kept passing barriers while wave 0's breadcrumbs stopped,
+// i.e. wave 0 ran on with an empty EXEC mask.
+#ifndef TSW_PBAR
+#define PBAR() __syncthreads()
+#else
+#define PBAR()                                                                                            \
+  do {                                                                                                    \
+    if (PLAN_DBG) {                                                                                       \
+      uint32_t* bid_ = bar_ids();                                                                         \
+      if ((threadIdx.x & 63u) == 0u) {                                                                    \
+        bid_[threadIdx.x >> 6] = __LINE__;                                                                \
+        if (P.hflags)                                                                                     \
+          __hip_atomic_store(&P.hflags[8u + (threadIdx.x >> 6)], (uint32_t)__LINE__, __ATOMIC_RELAXED,    \
+                             __HIP_MEMORY_SCOPE_SYSTEM);                                                  \
+      }                                                                                                   \
+      __syncthreads();                                                                                    \
+      if ((threadIdx.x & 63u) == 0u && P.hflags) {                                                        \
+        __hip_atomic_store(&P.hflags[8u + (threadIdx.x >> 6)], 0x10000u | (uint32_t)__LINE__,             \
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                                  \
+        __hip_atomic_fetch_add(&P.hflags[24u + (threadIdx.x >> 6)], 1u, __ATOMIC_RELAXED,                 \
+                               __HIP_MEMORY_SCOPE_SYSTEM);                                                \
+      }                                                                                                   \
+      if (threadIdx.x == 0u) {                                                                            \
+        for (uint32_t w_ = 1; w_ < (blockDim.x >> 6); ++w_)                                               \
+          if (bid_[w_] != bid_[0] && bid_[16] == 0u) {                                                    \
+            bid_[16] = 1u;                                                                                \
+            if (P.hflags)                                                                                 \
+              __hip_atomic_store(&P.hflags[4], (bid_[0] << 16) | bid_[w_], __ATOMIC_RELAXED,              \
+                                 __HIP_MEMORY_SCOPE_SYSTEM);                                              \
+            printf("[k_plan] barrier mismatch: wave 0 at line %u, wave %u at line %u\n", bid_[0], w_, bid_[w_]); \
+          }                                                                                               \
+      }                                                                                                   \
+      __syncthreads();                                                                                    \
+    } else {                                                                                              \
+      __syncthreads();                                                                                    \
+    }                                                                                                     \
+  } while (0)
+#endif
 
 namespace tsw {
 
 namespace {
+
+__device__ __forceinline__ uint32_t* bar_ids() {  // PBAR: per-wave barrier line, [16] = reported
+  __shared__ uint32_t b[17];
+  return b;
+}
 
 constexpr uint8_t NHC_DIRTY = 0xFE;  // per-agent next-hop code must be re-looked-up
 constexpr uint32_t OCC_NONE = 0xFFFFFFFFu;
@@ -192,12 +238,12 @@ __device__ void rules_init(const PlanArgs& P, const Arrays& S, uint32_t* pf = nu
     S.F1[n] = n;
     S.F2[n] = n;
   }
-  __syncthreads();
+  PBAR();
   uint32_t* a = S.F1;
   uint32_t* b = S.F2;
   for (uint32_t r = 1; r <= n; r <<= 1) {
     for (uint32_t k = tid; k < n; k += bd) b[k] = a[a[k]];
-    __syncthreads();
+    PBAR();
     uint32_t* t = a;
     a = b;
     b = t;
@@ -206,7 +252,7 @@ __device__ void rules_init(const PlanArgs& P, const Arrays& S, uint32_t* pf = nu
     const uint32_t c = a[k];
     if (c != n) S.ONC[c] = 1;
   }
-  __syncthreads();
+  PBAR();
 }
 
 // Incremental rules relabel (thread 0) after a firing changed the goals of the `cnt` agents in
@@ -356,7 +402,7 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
                                   uint32_t sec) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   if (tid == 0) *s_need = 0;
-  __syncthreads();
+  PBAR();
   for (uint32_t k = tid; k < P.n; k += bd) {
     if (S.NHC[k] <= NH_STAY) continue;
     const uint32_t v = S.V[k], g = S.G[k];
@@ -381,7 +427,7 @@ __device__ uint32_t refresh_codes(const PlanArgs& P, const Arrays& S, uint32_t* 
       atomicAdd(s_need, 1u);
     }
   }
-  __syncthreads();
+  PBAR();
   return *s_need;
 }
 
@@ -459,7 +505,7 @@ __device__ int coop_wait(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint
       P.cc->dbg_depth_max = max(P.cc->dbg_depth_max, dep);
     }
   }
-  __syncthreads();
+  PBAR();
   const unsigned long long t0 = wall_clock64();
   int st = COOP_OK;
   for (uint32_t k = tid; k < P.n && st == COOP_OK; k += bd) {
@@ -493,7 +539,7 @@ __device__ int coop_wait(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint
     }
   }
   if (st != COOP_OK) atomicMax(s_flag, (uint32_t)(st == COOP_GIVE_UP ? 3 : st));
-  __syncthreads();
+  PBAR();
   const uint32_t f = *s_flag;
   if (tid == 0) {
     const unsigned long long dt = wall_clock64() - t0;
@@ -508,7 +554,7 @@ __device__ int coop_wait(const PlanArgs& P, const Arrays& S, uint32_t* s_q, uint
     P.cc->waits_sec[sec] += 1u;
     P.cc->wait_sec[sec] += dt;
   }
-  __syncthreads();
+  PBAR();
   return f == 3u ? COOP_GIVE_UP : (int)f;
 }
 
@@ -527,7 +573,7 @@ __device__ void coop_requeue(const PlanArgs& P, const Arrays& S, uint32_t* s_q) 
     const uint32_t qi = atomicAdd(&s_q[0], 1u);
     if (qi < P.qcap) put_query(P, p, qi, v, S.G[k], tab);
   }
-  __syncthreads();
+  PBAR();
 }
 
 // Next hops are missing (refresh_codes returned nonzero and queued them). Coop mode: wait for the
@@ -573,7 +619,7 @@ __device__ void rules_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* s_q
     const uint32_t vs = S.V[s];
     if (P.nh[(uint64_t)tab * P.nstride + vs] == NH_UNKNOWN) prefetch_pair(P, vs, S.G[k], tab, s_q);
   }
-  __syncthreads();
+  PBAR();
 }
 
 // rules_prefetch restricted to the agents a firing changed (rule 3: b and s, rule 4: the cycle):
@@ -627,7 +673,7 @@ __device__ void rules_prefetch_list(const PlanArgs& P, const Arrays& S, uint32_t
                                     uint32_t cnt) {
   const uint32_t tid = threadIdx.x, bd = blockDim.x;
   for (uint32_t i = tid; i < cnt; i += bd) prefetch_changed(P, S, s_q, lst[i]);
-  __syncthreads();
+  PBAR();
 }
 
 // The shortest-path DAG toward goal g past cell u (u's own pair is queued by the caller): whichever
@@ -783,7 +829,7 @@ __device__ void nextnext_prefetch(const PlanArgs& P, const Arrays& S, uint32_t* 
     if (P.wf) P.wf[k] = make_uint4(vk, gk, ue, he);
     if (left > 0u && dtab >= 0 && (P.prefetch_ext & 2u)) walk_prefetch(P, s_q, pc, dc, dtab, left);
   }
-  __syncthreads();
+  PBAR();
 }
 
 // Serial movement phase (tswap.rs:257-285) — used when cells are shared by several agents
@@ -859,11 +905,18 @@ __device__ bool walk_move(const PlanArgs& P, const Arrays& S, PlanCtl& ctl) {
 // access waits for every outstanding global load as well). Otherwise part_lds picks arrays at run time.
 template <bool AG, bool OC, bool MUL, bool PG>
 // PlanArgs lives in device memory (written by launch_plan before the dispatch) and is read through a
-// const restrict pointer: the kernel body's field loads are scalar loads, and the out-of-line helpers get
-// a reference to it instead of to a private copy (a by-value kernel argument whose address reaches a
-// non-inlined call is copied to scratch, and every field access then became a scratch load; round 6).
+// const restrict pointer, so the out-of-line helpers get a reference to it instead of to a private copy
+// (a by-value kernel argument whose address reaches a non-inlined call is copied to scratch, and every
+// field access then became a scratch load; round 6). Its field loads are vector loads the compiler
+// repeats after stores (each one a memory round trip and a wait): the fields read inside the rules and
+// movement rounds — the instrumentation switch above all, tested at every sub-step — are read once here.
+#undef PLAN_DBG
+#define PLAN_DBG (kdbg)
 __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restrict__ Pg, WorkerArgs Wk) {
   const PlanArgs& P = *Pg;
+  const bool kdbg = __builtin_amdgcn_readfirstlane(P.dbg) != 0u;
+  const uint32_t kab = __builtin_amdgcn_readfirstlane(P.ab_flags);
+  const uint32_t kwcap = __builtin_amdgcn_readfirstlane(P.walk_cap);
   extern __shared__ __align__(16) uint8_t smem[];
   if (blockIdx.x != 0) {  // coop mode: a K3 worker workgroup (tsw_worker.h), Wk.wpb single-wave workers
     const uint32_t w = threadIdx.x >> 6;
@@ -881,7 +934,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
   __shared__ uint64_t s_red[16];
   __shared__ uint64_t s_bestk[ABATCH];  // K4: per batch agent, block minimum of (distance, task) (LDS atomic min)
   __shared__ uint32_t s_apos[ABATCH], s_acct[ABATCH], s_cnt2, s_ub[ABATCH];
-  __shared__ unsigned long long s_tick[40], s_tlast, s_tp;
+  __shared__ unsigned long long s_tick[48], s_tlast, s_tp;
   __shared__ uint32_t s_tsec;
   __shared__ uint32_t s_bad;               // ASSIGN looked up an off-grid/blocked task cell
   __shared__ uint32_t s_nassign, s_npick;  // diagnostics: this step's assignments / pickup arrivals
@@ -1005,7 +1058,8 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
     s_q[8] = 0;  // predicted task chains queued this launch (coop mode)
     s_q[9] = 0;  // ... last published head
     if (P.coop) __hip_atomic_store(&P.cc->t_now, s_ctl.t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int k = 0; k < 40; ++k) s_tick[k] = 0;
+    for (int k = 0; k < 48; ++k) s_tick[k] = 0;
+    bar_ids()[16] = 0u;
     s_tlast = wall_clock64();
     s_tsec = 7;  // entry / copy-in
     // the host's watchdog: the planner block is resident
@@ -1013,7 +1067,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
       __hip_atomic_store(&P.hflags[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
-  __syncthreads();
+  PBAR();
   if (s_ctl.section == SEC_RULES || s_ctl.section == SEC_MOVE) {
     // resuming after K3 resolved the missing next hops: every code starts dirty here
     const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
@@ -1024,7 +1078,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
         s_exit = 1;
       }
     }
-    __syncthreads();
+    PBAR();
   }
 
   for (;;) {
@@ -1038,7 +1092,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
         s_ctl.status = PLAN_NEED_QUERIES;
         s_exit = 1;
       }
-      __syncthreads();
+      PBAR();
       break;
     }
     if (s_abort) {  // watchdog: exit with the position recorded in ctl (section, cursor, rounds)
@@ -1047,7 +1101,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
         P.ctl->err |= ERR_ABORT;
         s_exit = 1;
       }
-      __syncthreads();
+      PBAR();
       break;
     }
     const uint32_t sec = s_ctl.section;
@@ -1083,12 +1137,12 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           s_tick[39] += 1;  // diagnostics: ASSIGN sections (sub-phase ticks in [32..38])
         }
       }
-      __syncthreads();
+      PBAR();
       for (uint32_t base = 0; base < n && !s_bad; base += bd) {
         const uint32_t i = base + tid;
         bool idle = false;
         if (tid == 0) s_badat = NO_AGENT;  // lowest agent of this chunk with a bad delivery cell
-        __syncthreads();
+        PBAR();
         if (i < n) {
           uint8_t st = P.st[i];
           if (S.V[i] == S.G[i] && st != ST_IDLE) {
@@ -1119,7 +1173,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
         }
         const uint64_t bal = __ballot(idle);
         if (lane == 0) s_wcount[wid] = (uint32_t)__popcll(bal);
-        __syncthreads();
+        PBAR();
         PLAN_TICK(32);
         if (idle) {
           uint32_t off = 0;
@@ -1132,7 +1186,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           for (uint32_t w = 0; w < nwaves; ++w) c += s_wcount[w];
           s_cnt = c;
         }
-        __syncthreads();
+        PBAR();
         PLAN_TICK(33);
         const uint32_t cnt = s_cnt, bad_at = s_badat;
         // Assignments in batches of up to ABATCH agents (index order): one block-wide pass computes every
@@ -1143,7 +1197,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
         // so it IS the sequential first minimum (min_by_key, tswap.rs:125-130).
         // batch size adapts: it doubles after a batch without a conflict and drops to the accepted count
         // after one (the t = 0 burst of a dense instance conflicts often; a busy step's handful rarely)
-        uint32_t bcur = (P.ab_flags & 4u) ? 1u : ABATCH;
+        uint32_t bcur = (kab & 4u) ? 1u : ABATCH;
         for (uint32_t kk = 0; kk < cnt && !s_bad;) {
           const uint32_t B = min(bcur, cnt - kk);
           if (tid < B) {
@@ -1152,7 +1206,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
             s_bestk[tid] = ~0ull;
             s_ub[tid] = 0xFFFFFFFFu;
           }
-          __syncthreads();
+          PBAR();
           // Spatially pruned scan. The host orders the tasks along a Morton curve of their pickup points and
           // cuts that order into chunks of KCH entries with a bounding box each (static) and a count of
           // untaken entries (KCNT). Phase A: a chunk with an untaken entry holds one within
@@ -1201,7 +1255,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
             const uint32_t wm = __ockl_wfred_min_u32(ub[b]);
             if (lane == 0) atomicMin(&s_ub[b], wm);
           }
-          __syncthreads();
+          PBAR();
           uint32_t bdst[ABATCH], btsk[ABATCH];
 #pragma unroll
           for (uint32_t b = 0; b < ABATCH; ++b) {
@@ -1259,7 +1313,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
             if (lane == 0 && dm != 0xFFFFFFFFu)
               atomicMin(reinterpret_cast<unsigned long long*>(&s_bestk[b]), ((unsigned long long)dm << 32) | tm);
           }
-          __syncthreads();
+          PBAR();
           PLAN_TICK(34);
           if (tid == 0) {
             uint32_t acc = 0, stop = 0;
@@ -1283,7 +1337,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
               s_tick[38] += acc;  // agents accepted
             }
           }
-          __syncthreads();
+          PBAR();
           PLAN_TICK(35);
           const uint32_t acc = s_cnt2;
           if (tid < acc) {  // the accepted agents' updates in parallel (tswap.rs:132-136)
@@ -1334,18 +1388,18 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
               }
             }
           }
-          __syncthreads();
+          PBAR();
           PLAN_TICK(36);
           if (s_doit) break;  // block-uniform
           kk += acc;
-          bcur = (P.ab_flags & 4u) ? 1u : acc == B ? min(ABATCH, 2u * bcur) : max(acc, 1u);
+          bcur = (kab & 4u) ? 1u : acc == B ? min(ABATCH, 2u * bcur) : max(acc, 1u);
         }
         if (bad_at != NO_AGENT && !s_bad) {  // block-uniform
           if (tid == 0) {
             atomicOr(&P.ctl->err, ERR_BAD_DELIVERY);
             s_bad = 1;
           }
-          __syncthreads();
+          PBAR();
         }
       }
       if (P.t0_delay_ticks && s_ctl.t == 0u && tid == 0) {  // diagnostic A/B: workers get a head start
@@ -1357,14 +1411,14 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           s_ctl.status = PLAN_ERROR;
           s_exit = 1;
         }
-        __syncthreads();
+        PBAR();
         break;
       }
       if (tid == 0) {
         s_ctl.section = SEC_PRE1;
         s_ctl.i = 0;
       }
-      __syncthreads();
+      PBAR();
     } else if (sec == SEC_PRE1 || sec == SEC_PRE2) {
       if (sec == SEC_PRE1 && tid == 0) {
         // walk-ahead depth (coop): wide_hi (32) hops on grids up to 2^18 cells while the workers keep up
@@ -1419,14 +1473,14 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           s_ctl.status = PLAN_NEED_QUERIES;
           s_exit = 1;
         }
-        __syncthreads();
+        PBAR();
         break;
       }
       if (tid == 0) {
         s_ctl.section = sec == SEC_PRE1 ? SEC_RULES : SEC_MOVE;
         s_ctl.i = 0;
       }
-      __syncthreads();
+      PBAR();
     } else if (sec == SEC_RULES) {
       // ---- rules phase as "first firing agent" rounds (see header) ------------
       // Cycle labels ONC (k lies on a cycle of succ) come from pointer doubling once per
@@ -1740,7 +1794,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
               // rule 4 on a 2-cycle k <-> s (two agents meeting head on, the common firing in 1-wide aisles):
               // the rotation (tswap.rs:241-249) is the exchange of their goals, and each one's new next hop is
               // the other's CANDC — the code of (the cell it sits on, the goal it takes)
-              const bool r2 = !r3 && onck && !(P.ab_flags & 1u) && S.SUCC[sk] == k;
+              const bool r2 = !r3 && onck && !(kab & 1u) && S.SUCC[sk] == k;
               bool ok = (r3 && vk != p_gs) || r2;  // rule 3 without a shared start cell, or the 2-cycle
               if (ok && code > NH_STAY) code = p_tk >= 0 ? nh_code(P, p_tk, p_vs) : NH_UNKNOWN;
               ok = ok && code <= NH_STAY;
@@ -1819,19 +1873,27 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
               // the next firing lane's precomputation is stale: redo it for every stale candidate
               if (!__builtin_amdgcn_readlane((int)(pv ? 1u : 0u), (int)l)) precompute(f && !pv);
               prof(17);
-              if (AG && __builtin_amdgcn_readlane((int)(pv && !p_walk ? 1u : 0u), (int)l)) {
-                // ---- batch (agent arrays in LDS): the longest run of firing lanes from l whose rule-3 swaps cannot see each
-                // other. Firing lanes mark the agents their swap writes (b = k, s = sk) with their lane
-                // (LDS min). A lane whose own agent, successor or precomputed ns carries an earlier
-                // lane's mark reads state that earlier swap changes; the batch ends before the first
+              const bool walk_batch = !(kab & 8u);  // A/B (diagnostic build): walking firings one at a time
+              if (AG && __builtin_amdgcn_readlane((int)(pv && (walk_batch || !p_walk) ? 1u : 0u), (int)l)) {
+                // ---- batch (agent arrays in LDS): the longest run of firing lanes from l whose firings cannot see
+                // each other — rule-3 swaps and 2-cycle rotations (97 % of busy C3's firings) with their
+                // precomputation current. Firing lanes mark the agents they write (b = k, s = sk) with their
+                // lane (LDS min). A lane whose own agent, successor or precomputed ns carries an earlier
+                // lane's mark reads state that earlier firing changes; the batch ends before the first
                 // such lane (firing or not: a non-firing s may start firing) and before the first firing
-                // lane that is not a plain precomputed swap. The swaps of the batch then touch disjoint
-                // agents and read nothing another one writes, so applying them at once equals applying
-                // them in agent order (tswap.rs:180-252). Lanes past the batch that it touched reload.
+                // lane that is not a plain precomputed one. A firing that moves a successor (s's, and b's
+                // in a rotation) must not close a new cycle (its labels would change other agents'
+                // firing): every such lane walks its new successor chains at once, on the state before
+                // the batch plus its own change, as the serial path below does after its firing; a walk
+                // that closes a cycle, runs past P.walk_cap hops or passes an agent an earlier lane marked
+                // ends the batch at that lane. The firings of the batch then touch disjoint agents and
+                // read nothing another one writes, so applying them at once equals applying them in
+                // agent order (tswap.rs:180-252). Lanes past the batch that it touched reload.
                 const uint32_t k = base + lane;
                 const bool fire_l = ((m >> lane) & 1ull) != 0ull;  // m holds lanes >= l only
-                const bool simple = fire_l && pv && !p_walk;
-                if (simple) {
+                const bool cand = fire_l && pv && (walk_batch || !p_walk);
+                const bool r2 = cand && (p_code >> 16) != 0u;
+                if (cand) {
                   atomicMin(&S.MK[k], lane);
                   atomicMin(&S.MK[sk], lane);
                 }
@@ -1842,13 +1904,56 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
                   if (sk != SUCC_TERM) c = min(c, S.MK[sk]);
                   if (pv && p_ns != SUCC_TERM) c = min(c, S.MK[p_ns]);
                 }
-                const uint64_t bm = __ballot(lane >= l && (c < lane || (fire_l && !simple)));
+                prof(40);
+                bool simple = cand;
+                uint32_t cw = c;  // with the marks met on the walks
+                uint32_t hops = 0;  // diagnostics
+                if (cand && p_walk) {
+                  // walk from st along the successors after this lane's firing (o = the other agent whose
+                  // successor it changes, a rotation's b; its ONC label is cleared with the 2-cycle): 0 no
+                  // new cycle (TERM, a self-loop or a labelled agent ends the chain), 1 a cycle or too long
+                  auto walk = [&](uint32_t st, uint32_t first, uint32_t o, uint32_t o_next) -> uint32_t {
+                    if (first == SUCC_TERM || first == st) return 0u;
+                    uint32_t x = first;
+                    for (uint32_t it = 0; it < kwcap; ++it) {
+                      if (x == SUCC_TERM) return 0u;
+                      if (x == st) return 1u;
+                      cw = min(cw, S.MK[x]);
+                      ++hops;
+                      uint32_t nx;
+                      bool lab;
+                      if (x == o) {
+                        nx = o_next;
+                        lab = false;
+                      } else {
+                        nx = S.SUCC[x];
+                        lab = S.ONC[x] != 0;
+                      }
+                      if (lab || nx == x) return 0u;
+                      x = nx;
+                    }
+                    return 1u;
+                  };
+                  // rule 3: s was at its goal (terminal, unlabelled) and b keeps its successor s
+                  uint32_t bad = walk(sk, p_ns, r2 ? k : SUCC_TERM, p_nk);
+                  if (!bad && r2) bad = walk(k, p_nk, sk, p_ns);
+                  simple = !bad;
+                }
+                if (PLAN_DBG) {  // diagnostics: batches, longest walk of each
+                  const uint32_t mh = ~wave_min_u32(~hops);
+                  if (lane == 0) {
+                    s_tick[43] += 1;
+                    s_tick[44] += mh;
+                  }
+                }
+                prof(41);
+                const uint64_t bm = __ballot(lane >= l && (cw < lane || (fire_l && !simple)));
                 const uint32_t cut = bm ? (uint32_t)__builtin_ctzll(bm) : 64u;
                 const uint64_t batch = cut >= 64u ? m : (m & ((1ull << cut) - 1ull));
                 const bool inb = ((batch >> lane) & 1ull) != 0ull;
                 if (inb) {  // rule 3 (tswap.rs:198-202): b <-> s goals, s's new code and successor
-                  DTAG(k, 1u);
-                  DTAG(sk, 2u);
+                  DTAG(k, r2 ? 4u : 1u);
+                  DTAG(sk, r2 ? 4u : 2u);
                   S.G[k] = p_gs;
                   S.GT[k] = p_ts;
                   S.G[sk] = p_gk;
@@ -1857,43 +1962,54 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
                   S.CANDC[k] = NHC_DIRTY;
                   S.NHC[sk] = (uint8_t)p_code;
                   S.SUCC[sk] = p_ns;
+                  if (r2) {  // rule 4 on the 2-cycle (:241-249): the same exchange, b's new code and successor
+                    S.NHC[k] = (uint8_t)(p_code >> 8);
+                    S.SUCC[k] = p_nk;
+                    S.ONC[k] = 0;
+                    S.ONC[sk] = 0;
+                  }
                 }
                 const bool touched = lane >= cut && c < cut;
                 __threadfence_block();
-                if (simple) {
+                if (cand) {
                   S.MK[k] = 0xFFFFFFFFu;
                   S.MK[sk] = 0xFFFFFFFFu;
                 }
                 __threadfence_block();
-                if (touched && k < n) {  // exact state after the batch, from LDS
-                  sk = S.SUCC[k];
-                  onck = S.ONC[k] != 0;
-                  f = sk != SUCC_TERM && sk != k && (S.V[sk] == S.G[sk] || onck);
-                  pv = false;
-                }
-                // b and s of every swap join the changed list (targeted prefetch at the next relabel)
-                const uint32_t nb = (uint32_t)__popcll(batch);
-                if (nc != NO_AGENT && nc + 2u * nb <= LIST_CAP) {
-                  if (inb) {
-                    const uint32_t r = lane_rank(batch);
-                    list[nc + 2u * r] = k;
-                    list[nc + 2u * r + 1u] = sk;
+                prof(42);
+                // an empty batch (lane l's own walk closed a cycle or ran long): lane l fires on the serial path
+                if (batch != 0ull) {
+                  if (PLAN_DBG && lane == 0) s_tick[11] += (uint32_t)__popcll(__ballot(inb && r2));  // rule-4 rotations
+                  if (touched && k < n) {  // exact state after the batch, from LDS
+                    sk = S.SUCC[k];
+                    onck = S.ONC[k] != 0;
+                    f = sk != SUCC_TERM && sk != k && (S.V[sk] == S.G[sk] || onck);
+                    pv = false;
                   }
-                  nc += 2u * nb;
-                } else {
-                  nc = NO_AGENT;
+                  // b and s of every swap join the changed list (targeted prefetch at the next relabel)
+                  const uint32_t nb = (uint32_t)__popcll(batch);
+                  if (nc != NO_AGENT && nc + 2u * nb <= LIST_CAP) {
+                    if (inb) {
+                      const uint32_t r = lane_rank(batch);
+                      list[nc + 2u * r] = k;
+                      list[nc + 2u * r + 1u] = sk;
+                    }
+                    nc += 2u * nb;
+                  } else {
+                    nc = NO_AGENT;
+                  }
+                  rr += nb;
+                  const uint32_t last = 63u - (uint32_t)__builtin_clzll(batch);
+                  if (lane == last) {
+                    s_best = k;
+                    s_miss = 0;
+                    s_ctl.i = k + 1u;
+                  }
+                  m = last == 63u ? 0ull : (__ballot(f) & ~((2ull << last) - 1ull));
+                  if (PLAN_DBG && lane == 0) s_tick[23] += nb;
+                  prof(18);
+                  continue;
                 }
-                rr += nb;
-                const uint32_t last = 63u - (uint32_t)__builtin_clzll(batch);
-                if (lane == last) {
-                  s_best = k;
-                  s_miss = 0;
-                  s_ctl.i = k + 1u;
-                }
-                m = last == 63u ? 0ull : (__ballot(f) & ~((2ull << last) - 1ull));
-                if (PLAN_DBG && lane == 0) s_tick[23] += nb;
-                prof(18);
-                continue;
               }
               uint32_t r_fl = 0, r_s = 0, r_ns = 0, r_bits = 0;
               const bool fast = __builtin_amdgcn_readlane((int)(pv ? 1u : 0u), (int)l) != 0;
@@ -2102,7 +2218,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           }
           best = wave_min_u32(best);
           if (lane == 0) s_wcount[wid] = best;
-          __syncthreads();
+          PBAR();
           PLAN_TICK(13);
           if (tid == 0) {
             uint32_t b = NO_AGENT;
@@ -2116,7 +2232,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
             }
           }
         }
-        __syncthreads();
+        PBAR();
         PLAN_TICK(14);
         if (s_best == NO_AGENT) break;
         if (tid == 0 && (s_ctl.rule_rounds & 1023u) == 1023u && plan_abort(P)) s_abort = 1;
@@ -2129,7 +2245,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
               s_ctl.status = PLAN_NEED_QUERIES;
               s_exit = 1;
             }
-            __syncthreads();
+            PBAR();
             break;
           }
           // only the agents in `list` changed since the last labelling: relabel incrementally when
@@ -2140,7 +2256,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
               s_flag = ok ? 1u : 0u;
               if (ok) s_ctl.relabel_inc += 1;
             }
-            __syncthreads();
+            PBAR();
             if (!s_flag) {
               rules_init(P, S);
               if (tid == 0) s_ctl.relabel_full += 1;
@@ -2149,7 +2265,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
             rules_init(P, S);
             if (tid == 0) s_ctl.relabel_full += 1;
           }
-          __syncthreads();
+          PBAR();
           if (P.prefetch) {
             if (P.wide_prefetch && s_cnt != NO_AGENT) rules_prefetch_list(P, S, s_q, list, s_cnt);
             else rules_prefetch(P, S, s_q);
@@ -2164,18 +2280,18 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
       // agents the phase changed since the last relabel (fast rule-3 swaps and 2-cycle rotations never
       // take the relabel path): their new paths walked ahead and their rules candidates queued now, as
       // the relabel path does — the movement phase and the next step read them
-      if (P.prefetch && s_cnt != 0u && !(P.ab_flags & 2u)) {
+      if (P.prefetch && s_cnt != 0u && !(kab & 2u)) {
         if (P.wide_prefetch && s_cnt != NO_AGENT) rules_prefetch_list(P, S, s_q, list, s_cnt);
         else rules_prefetch(P, S, s_q);
         if (P.coop && tid == 0) coop_publish(P, s_q);
-        __syncthreads();
+        PBAR();
       }
       if (tid == 0) {
         s_ctl.section = SEC_PRE2;
         s_ctl.i = 0;
         s_cnt = 0;
       }
-      __syncthreads();
+      PBAR();
     } else if (sec == SEC_MOVE && P.has_dups) {
       if (tid == 0) {
         s_ctl.miss = 0;
@@ -2185,12 +2301,12 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
         }
         if (s_ctl.miss == 2) atomicOr(&P.ctl->err, ERR_NO_TABLE);
       }
-      __syncthreads();
+      PBAR();
       if (s_ctl.miss) {
         const uint32_t q = refresh_codes(P, S, s_q, &s_need, s_ctl.section);
         if (s_ctl.miss == 1 && q > 0 && coop_resolve(P, S, s_q, &s_need, &s_flag, s_ctl.section)) {
           if (tid == 0) s_ctl.miss = 0;
-          __syncthreads();
+          PBAR();
           continue;  // resume the serial scan at ctl.i
         }
         if (tid == 0) {
@@ -2198,14 +2314,14 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           s_ctl.status = (q > 0 && s_q[0] > 0 && s_ctl.miss == 1) ? PLAN_NEED_QUERIES : PLAN_ERROR;
           s_exit = 1;
         }
-        __syncthreads();
+        PBAR();
         break;
       }
     } else if (sec == SEC_MOVE) {
       // ---- movement phase as decidability rounds (see header) -----------------
       if (s_ctl.i == 0) {
         for (uint32_t k = tid; k < n; k += bd) S.DEC[k] = (S.V[k] == S.G[k]) ? DEC_DONE : DEC_OPEN;
-        __syncthreads();
+        PBAR();
         if (tid == 0) s_ctl.i = 1;  // DEC initialised for this step (survives relaunches)
       }
       // Round passes as per-agent bodies, run either block-wide (k = tid, tid + bd, ...) or, in
@@ -2329,12 +2445,12 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           if (PLAN_DBG) s_tp = wall_clock64();
           if ((s_ctl.move_rounds & 1023u) == 0u && plan_abort(P)) s_abort = 1;
         }
-        __syncthreads();
+        PBAR();
         if (s_abort) break;
         set_tag(s_ctl.move_rounds);
         if (MUL && tag16 == 1u && s_ctl.move_rounds > 1u) {  // the 16-bit tag wrapped: old entries would match
           for (uint32_t c = tid; c < P.ncell; c += bd) S.MU32[c] = 0u;
-          __syncthreads();
+          PBAR();
         }
         int open = 0;
         for (uint32_t k = tid; k < n; k += bd) open |= pass1(k) ? 1 : 0;
@@ -2347,22 +2463,22 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           // compact the open agents (index order) into `list` for the wave tail
           const uint64_t bal = __ballot(open != 0);
           if (lane == 0) s_wcount[wid] = (uint32_t)__popcll(bal);
-          __syncthreads();
+          PBAR();
           if (open) {
             uint32_t off = 0;
             for (uint32_t w = 0; w < wid; ++w) off += s_wcount[w];
             list[off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = tid;
           }
-          __syncthreads();
+          PBAR();
           tail = true;
           break;
         }
         for (uint32_t k = tid; k < n; k += bd) pass2(k);
-        __syncthreads();
+        PBAR();
         PLAN_TICK(10);
         const uint32_t spmin = s_best;
         for (uint32_t k = tid; k < n; k += bd) pass3(k, spmin);
-        __syncthreads();
+        PBAR();
         PLAN_TICK(12);
         if (s_miss) break;
       }
@@ -2404,7 +2520,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
             if (kk != NO_AGENT && S.DEC[kk] != DEC_OPEN) kk = NO_AGENT;  // committed: leaves the tail
           }
         }
-        __syncthreads();
+        PBAR();
       }
       if (s_abort) continue;  // watchdog: exit at the top of the section loop, position kept
       if (s_miss) {
@@ -2415,14 +2531,14 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           s_ctl.status = s_q[0] > 0 ? PLAN_NEED_QUERIES : PLAN_ERROR;
           s_exit = 1;
         }
-        __syncthreads();
+        PBAR();
         break;
       }
       if (tid == 0) {
         s_ctl.section = SEC_RECORD;
         s_ctl.i = 0;
       }
-      __syncthreads();
+      PBAR();
     } else if (sec == SEC_RECORD) {
       if (P.mode == MODE_STEP) {
         if (tid == 0) {
@@ -2431,7 +2547,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           s_ctl.qcount = s_q[0];  // speculative prefetches still queued: the host resolves them
           s_exit = 1;
         }
-        __syncthreads();
+        PBAR();
         break;
       }
       // ---- record (tswap.rs:144-158) + termination (tswap.rs:163-169) --------
@@ -2467,14 +2583,14 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           s_ctl.section = SEC_ASSIGN;
         }
       }
-      __syncthreads();
+      PBAR();
     } else {
       break;  // SEC_DONE
     }
   }
 
   // ---- write back ------------------------------------------------------------
-  __syncthreads();
+  PBAR();
   if constexpr (AG)
     for (uint32_t k = tid; k < n; k += bd) {
       P.v[k] = S.V[k];
@@ -2499,9 +2615,11 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
     P.ctl->err |= err;
     s_tick[s_tsec] += wall_clock64() - s_tlast;
     if (P.sec_ticks)
-      for (int k = 0; k < 40; ++k) P.sec_ticks[k] += s_tick[k];
+      for (int k = 0; k < 48; ++k) P.sec_ticks[k] += s_tick[k];
   }
 }
+#undef PLAN_DBG
+#define PLAN_DBG (P.dbg != 0u)
 
 
 template <bool AG, bool OC, bool MUL, bool PG = false>
