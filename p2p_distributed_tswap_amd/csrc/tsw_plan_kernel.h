@@ -156,15 +156,18 @@ struct Arrays {
 // after a worker has stored the code (coop mode): then the word is read again at agent scope, so a
 // code that is already known does not send the planner through a refresh pass and a wait. Codes never
 // change once written, so either read is exact.
-__device__ __forceinline__ uint8_t nh_code(const PlanArgs& P, int32_t tab, uint32_t v) {
-  const uint8_t* p = P.nh + (uint64_t)tab * P.nstride + v;
+__device__ __forceinline__ uint8_t nh_code_at(const uint8_t* nh, uint64_t nstride, bool coop, int32_t tab, uint32_t v) {
+  const uint8_t* p = nh + (uint64_t)tab * nstride + v;
   uint8_t c = *p;
-  if (P.coop && (c == NH_PENDING || c == NH_PENDING_S)) {
+  if (coop && (c == NH_PENDING || c == NH_PENDING_S)) {
     const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3u),
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     c = (uint8_t)(w >> (8u * (uint32_t)((uintptr_t)p & 3u)));
   }
   return c;
+}
+__device__ __forceinline__ uint8_t nh_code(const PlanArgs& P, int32_t tab, uint32_t v) {
+  return nh_code_at(P.nh, P.nstride, P.coop != 0u, tab, v);
 }
 
 // next-hop code of agent k for its current (v, g); -1 unresolved, -2 goal has no table
@@ -917,6 +920,10 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
   const bool kdbg = __builtin_amdgcn_readfirstlane(P.dbg) != 0u;
   const uint32_t kab = __builtin_amdgcn_readfirstlane(P.ab_flags);
   const uint32_t kwcap = __builtin_amdgcn_readfirstlane(P.walk_cap);
+  const uint8_t* const knh = P.nh;  // next-hop tables, read by the rules rounds' swaps and rotations
+  const uint64_t kns = P.nstride;
+  const bool kcoop = P.coop != 0u;
+  auto nh_code_k = [&](int32_t tab, uint32_t v) { return nh_code_at(knh, kns, kcoop, tab, v); };
   extern __shared__ __align__(16) uint8_t smem[];
   if (blockIdx.x != 0) {  // coop mode: a K3 worker workgroup (tsw_worker.h), Wk.wpb single-wave workers
     const uint32_t w = threadIdx.x >> 6;
@@ -1444,7 +1451,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           const uint32_t tg = P.dtag[k] & 63u;
           P.dtag[k] = 0u;
           if (S.NHC[k] <= NH_STAY || S.V[k] == S.G[k] || S.GT[k] < 0) continue;
-          const uint8_t c = nh_code(P, S.GT[k], S.V[k]);
+          const uint8_t c = nh_code_k(S.GT[k], S.V[k]);
           if (c == NH_UNKNOWN || c == NH_PENDING) atomicAdd(&P.cc->dbg_tag[0][tg], 1u);
           else if (c == NH_PENDING_S) atomicAdd(&P.cc->dbg_tag[1][tg], 1u);
         }
@@ -1548,7 +1555,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           DTAG(b, 1u);
           DTAG(s, 2u);
           uint32_t code = candc;
-          if (code > NH_STAY && tb >= 0) code = nh_code(P, tb, vs);  // s's new goal is gb
+          if (code > NH_STAY && tb >= 0) code = nh_code_k(tb, vs);  // s's new goal is gb
           S.G[b] = gs;
           S.GT[b] = ts;
           S.G[s] = gb;
@@ -1656,7 +1663,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
           uint8_t code = S.CANDC[pa];
           if (code > NH_STAY) {
             const int32_t tab = S.GT[a];
-            code = tab >= 0 ? nh_code(P, tab, S.V[a]) : NH_UNKNOWN;
+            code = tab >= 0 ? nh_code_k(tab, S.V[a]) : NH_UNKNOWN;
           }
           if (code <= NH_STAY) S.NHC[a] = code;
           else bad = true;
@@ -1683,7 +1690,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
               S.SUCC[a] = sa;
               S.ONC[a] = (uint8_t)(2u + lane);
               const int32_t ta = S.GT[a];
-              if (sa != SUCC_TERM && sa != a && ta >= 0) cc = P.nh[(uint64_t)ta * P.nstride + S.V[sa]];
+              if (sa != SUCC_TERM && sa != a && ta >= 0) cc = knh[(uint64_t)ta * kns + S.V[sa]];
             }
             wave_order();
             __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -1796,12 +1803,12 @@ __global__ void __launch_bounds__(PLAN_BLOCK_MAX) k_plan(const PlanArgs* __restr
               // the other's CANDC — the code of (the cell it sits on, the goal it takes)
               const bool r2 = !r3 && onck && !(kab & 1u) && S.SUCC[sk] == k;
               bool ok = (r3 && vk != p_gs) || r2;  // rule 3 without a shared start cell, or the 2-cycle
-              if (ok && code > NH_STAY) code = p_tk >= 0 ? nh_code(P, p_tk, p_vs) : NH_UNKNOWN;
+              if (ok && code > NH_STAY) code = p_tk >= 0 ? nh_code_k(p_tk, p_vs) : NH_UNKNOWN;
               ok = ok && code <= NH_STAY;
               uint32_t code2 = 0, nk = SUCC_TERM;
               if (ok && r2) {
                 code2 = S.CANDC[sk];
-                if (code2 > NH_STAY) code2 = p_ts >= 0 ? nh_code(P, p_ts, vk) : NH_UNKNOWN;
+                if (code2 > NH_STAY) code2 = p_ts >= 0 ? nh_code_k(p_ts, vk) : NH_UNKNOWN;
                 ok = code2 <= NH_STAY;
                 if (ok && vk != p_gs) {  // k's new successor (k takes s's goal; at it when vk == p_gs)
                   const uint32_t oc = S.OCC[step_cell(vk, code2, W)];
