@@ -53,7 +53,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md ("HBM: 8 TB/s peak")
-PROFILE_TAG = "r5"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
+PROFILE_TAG = "r6"     # profiles/<tag>/pmc.json: PMC traffic per workload (scripts/profile_round.sh)
 BFS_WORKLOAD = "bfs:den520d_10k"
 
 

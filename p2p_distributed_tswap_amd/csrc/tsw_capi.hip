@@ -91,7 +91,7 @@ struct Tunables {
   int worker_fb = -1;             // TSW_WORKER_FB=0 / 1: global-g-score workers without / with the staged free bitmap (-1: by waves per CU)
   bool dag_exit = true;           // TSW_DAG_EXIT=0: coop workers' A* runs to the goal's pop (no DAG early exit)
   uint32_t dag_mask = 0;          // TSW_DAG_MASK: the DAG early-exit test runs every (mask + 1) pops (0: auto)
-  uint32_t ab_flags = 0;          // TSW_AB_FLAGS (A/B): 1 no 2-cycle fast path, 2 no end-of-rules prefetch, 4 one agent per K4 batch
+  uint32_t ab_flags = 0;          // TSW_AB_FLAGS (A/B): 1 no 2-cycle fast path, 2 no end-of-rules prefetch, 4 one agent per K4 batch, 8 no batched rules walks
   uint32_t t0_delay_us = 0;       // TSW_T0_DELAY_US (A/B): the planner idles this long after step 0's assignment
   uint32_t stale_steps = 16;      // TSW_SPEC_STALE: coop workers drop speculative pairs older than this many steps (0: never)
   uint32_t reg_heap = 63;         // TSW_ASTAR_REGHEAP: worker A* heaps up to this many entries in registers (0: LDS only)
