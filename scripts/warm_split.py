@@ -35,6 +35,15 @@ def plan_dispatches(d, counter):
     return rows
 
 
+def same_sources(product_id, diag_id) -> bool:
+    """The no-chains pass runs the diagnostic library, whose build id hashes the flavour too:
+    accept the pair when both ids are this tree's product / diagnostic hashes."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from __graft_entry__ import source_hash
+
+    return str(product_id) == source_hash("") and str(diag_id) == source_hash("diag")
+
+
 def main():
     fdir, wdir, warm_json, out_path = sys.argv[1:5]
     nc = sys.argv[5:8] if len(sys.argv) >= 8 else None
@@ -59,7 +68,7 @@ def main():
             raise SystemExit(f"no-chains: expected 3 k_plan dispatches per pass, got {len(fe2)} / {len(wr2)}")
         with open(nc[2]) as fh:
             wj2 = json.loads([l for l in fh if l.startswith("{")][-1])
-        if wj2.get("build_id") != wj.get("build_id"):
+        if wj2.get("build_id") != wj.get("build_id") and not same_sources(wj.get("build_id"), wj2.get("build_id")):
             raise SystemExit("no-chains profile of another build")
         planner = 2.0 * fe2[2][1] * 1024.0 + wr2[2][1] * 1024.0
         planner_src = "warm plan dispatch without task chains (diagnostic library, TSW_TASK_CHAINS=0)"
