@@ -30,3 +30,5 @@ def test_bench_two_ranks_gloo_one_gpu():
     assert isinstance(d["build_id"], str)
     assert d["config"]["timesteps_moving"] >= 1990
     assert d["bfs"]["sharded_build_allgather_ms"] is not None
+    # the same-N local build the sharded form is compared against
+    assert d["bfs"]["local_build_all_goals_ms"] is not None
