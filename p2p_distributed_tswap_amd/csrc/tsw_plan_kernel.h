@@ -13,7 +13,10 @@
 //                       back to k; Floyd walk on the LDS succ array)
 //             block-min -> first firing agent; one lane applies its goal swap /
 //             target rotation (:199-202, :241-249); cursor moves past it.
-//           Agents that do not fire change nothing, so this equals the sequential scan.
+//           Agents that do not fire change nothing, so this equals the sequential scan. With
+//           n <= wave_rules_max wave 0 runs the rounds alone, and a run of firings that touch
+//           disjoint agents (rule-3 swaps, 2-cycle rotations, none closing a new cycle) is
+//           applied as one batch (round 6).
 //   PRE2    parallel lookup for agents whose goal changed
 //   MOVE    movement phase (tswap.rs:257-285), exact, as decidability rounds: agent k
 //           commits in a round iff no still-undecided agent a < k can change what k reads
