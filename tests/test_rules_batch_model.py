@@ -119,7 +119,7 @@ def fire_one(world, V, G, occ, i):
     return False
 
 
-def rules_batched(world, V, G, walk_cap=16):
+def rules_batched(world, V, G, walk_cap=16, close_in_batch=False):
     """The kernel's wave rules loop with batches (see module docstring). Returns (goals, batched, serial)."""
     n = len(V)
     G = list(G)
@@ -196,7 +196,7 @@ def rules_batched(world, V, G, walk_cap=16):
                 for k in cand:
                     for a in (k, sk[k]):
                         MK[a] = min(MK.get(a, 1 << 30), k)
-                cut = None
+                cut, closed = None, False
                 c_of = {}
                 for k in lanes:  # every lane's marks of its own agent, successor and precomputed ns
                     c = min(MK.get(k, 1 << 30), MK.get(sk[k], 1 << 30) if sk[k] != TERM else 1 << 30)
@@ -209,31 +209,35 @@ def rules_batched(world, V, G, walk_cap=16):
                         continue
                     c = c_of[k]
                     p = pre.get(k) if fire[k] else None
-                    cw, simple = c, p is not None
+                    cw, simple, closing = c, p is not None, False
                     if simple and p["walk"]:
-                        def walk(st, first, o, o_next):
+                        def walk(st, first, o, o_next):  # 0 no new cycle, 1 a new cycle, 2 too long
                             nonlocal cw
                             if first in (TERM, st):
-                                return False
+                                return 0
                             x = first
                             for _ in range(walk_cap):
                                 if x == TERM:
-                                    return False
+                                    return 0
                                 if x == st:
-                                    return True
+                                    return 1
                                 cw = min(cw, MK.get(x, 1 << 30))
                                 nx, lab = (o_next, False) if x == o else (SUCC[x], ONC[x] != 0)
                                 if lab or nx == x:
-                                    return False
+                                    return 0
                                 x = nx
-                            return True
+                            return 2
                         s = sk[k]
                         bad = walk(s, p["ns"], k if p["r2"] else TERM, p["nk"])
-                        if not bad and p["r2"]:
+                        if bad == 0 and p["r2"]:
                             bad = walk(k, p["nk"], s, p["ns"])
-                        simple = not bad
+                        closing = bad == 1 and close_in_batch
+                        simple = bad == 0 or closing
                     if cw < k or (fire[k] and not simple):
                         cut = k
+                        break
+                    if fire[k] and closing:  # a firing that closes a new cycle ends the batch, included
+                        cut, closed = k + 1, True
                         break
                 batch = [k for k in firing if cut is None or k < cut]
                 if batch:
@@ -245,6 +249,10 @@ def rules_batched(world, V, G, walk_cap=16):
                             SUCC[k] = p["nk"]
                             ONC[k] = ONC[s] = 0
                     batched += len(batch)
+                    if closed:  # the last member closed a cycle: label it and rescan past the batch
+                        ONC = labels(SUCC)
+                        restart = batch[-1] + 1
+                        break
                     cut_v = n + 64 if cut is None else cut
                     for k in lanes:  # lanes past the batch that it touched reload
                         if k >= cut_v and c_of.get(k, 1 << 30) < cut_v:
@@ -299,6 +307,19 @@ def test_batched_rules_batch_most_firings():
         tot_b += b
         tot_s += s
     assert tot_b > tot_s  # the model exercises the batch path, not only the serial fallback
+
+
+def test_cycle_closing_firings_in_batch_are_exact():
+    """The measured-null extension (round 6, profiles/r6/ab_r6_close_in_batch.txt): a firing that closes a
+    new cycle joins the batch as its last member, its cycle is labelled and the scan resumes past it.
+    Exact in the model (and on the 262 GPU tests when it was built); not adopted for speed."""
+    tb = ts = 0
+    for seed in range(70, 110):
+        world, V, G = _state(seed, w=20, h=12, fill=0.6)
+        got, b, s = rules_batched(world, V, G, close_in_batch=True)
+        assert got == rules_sequential(world, V, G)
+        tb, ts = tb + b, ts + s
+    assert ts * 20 < tb  # nearly every firing batched
 
 
 @pytest.mark.parametrize("cap", [1, 2, 64])
